@@ -1,0 +1,172 @@
+"""ctypes binding of the C ABI in ``include/e2sar_hip.h``.
+
+The shared library ``e2sar_amd/lib/libe2sar_hip.so`` is built in-tree by
+``make`` (or ``__graft_entry__.build()``).  Loading fails loudly when it is
+missing: there is no CPU fallback for the SAR path.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libe2sar_hip.so")
+
+# status codes = -(E2SARErrorc) (reference include/e2sarError.hpp:23-39)
+OK = 0
+ERR_PARAMETER = -3
+ERR_OUT_OF_RANGE = -5
+ERR_NOT_FOUND = -7
+ERR_MEMORY = -10
+ERR_LOGIC = -11
+ERR_SYSTEM = -12
+ERR_DATA = -13
+
+LBRE_HDR_LEN = 36
+RE_HDR_LEN = 20
+LB_HDR_LEN = 16
+
+
+class SegEvent(C.Structure):
+    _fields_ = [
+        ("data", C.c_uint64),
+        ("eventNum", C.c_uint64),
+        ("lbTick", C.c_uint64),
+        ("bytes", C.c_uint32),
+        ("pktBase", C.c_uint32),
+        ("dataId", C.c_uint16),
+        ("entropy", C.c_uint16),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class ReasConfig(C.Structure):
+    _fields_ = [
+        ("withLBHeader", C.c_int),
+        ("tableSlots", C.c_uint32),
+        ("queueCapacity", C.c_uint32),
+        ("lostCapacity", C.c_uint32),
+        ("arenaBytes", C.c_uint64),
+    ]
+
+
+class EventRec(C.Structure):
+    _fields_ = [
+        ("eventNum", C.c_uint64),
+        ("arenaOffset", C.c_uint64),
+        ("bytes", C.c_uint32),
+        ("dataId", C.c_uint16),
+        ("flags", C.c_uint16),
+        ("numFragments", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class LostRec(C.Structure):
+    _fields_ = [
+        ("eventNum", C.c_uint64),
+        ("numFragments", C.c_uint64),
+        ("dataId", C.c_uint16),
+        ("enqueueLoss", C.c_uint16),
+        ("reserved", C.c_uint32),
+    ]
+
+
+class ReasStats(C.Structure):
+    _fields_ = [
+        ("enqueueLoss", C.c_uint64),
+        ("reassemblyLoss", C.c_uint64),
+        ("eventSuccess", C.c_uint64),
+        ("totalPackets", C.c_uint64),
+        ("totalBytes", C.c_uint64),
+        ("badHeaderDiscards", C.c_uint64),
+        ("dataErrCnt", C.c_uint64),
+        ("inProgress", C.c_int64),
+        ("completedPending", C.c_uint64),
+        ("lostPending", C.c_uint64),
+        ("arenaUsed", C.c_uint64),
+        ("tableUsed", C.c_uint64),
+        ("errorFlags", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
+assert C.sizeof(SegEvent) == 40
+assert C.sizeof(EventRec) == 32
+assert C.sizeof(LostRec) == 24
+
+vp = C.c_void_p
+u8p = C.c_void_p
+i = C.c_int
+u32 = C.c_uint32
+u64 = C.c_uint64
+sz = C.c_size_t
+
+# name -> (restype, argtypes); this list is also the export contract checked by tests
+SIGNATURES = {
+    "e2sar_hip_abi_version": (i, []),
+    "e2sar_hip_last_error": (C.c_char_p, []),
+    "e2sar_hip_ctx_create": (i, [i, vp, C.POINTER(vp)]),
+    "e2sar_hip_ctx_destroy": (None, [vp]),
+    "e2sar_hip_ctx_stream": (vp, [vp]),
+    "e2sar_hip_ctx_device": (i, [vp]),
+    "e2sar_hip_ctx_sync": (i, [vp]),
+    "e2sar_hip_device_alloc": (i, [vp, sz, C.POINTER(vp)]),
+    "e2sar_hip_device_free": (i, [vp, vp]),
+    "e2sar_hip_host_alloc": (i, [sz, C.POINTER(vp)]),
+    "e2sar_hip_host_free": (i, [vp]),
+    "e2sar_hip_memcpy_h2d": (i, [vp, vp, vp, sz]),
+    "e2sar_hip_memcpy_d2h": (i, [vp, vp, vp, sz]),
+    "e2sar_hip_memset_d": (i, [vp, vp, i, sz]),
+    "e2sar_hip_total_hdr_len": (sz, [i]),
+    "e2sar_hip_max_pld_len": (sz, [u32, i]),
+    "e2sar_hip_num_packets": (sz, [sz, sz]),
+    "e2sar_hip_packet_stride": (u32, [sz]),
+    "e2sar_hip_seg_plan": (i, [C.POINTER(SegEvent), u32, sz, C.POINTER(u32), C.POINTER(u32)]),
+    "e2sar_hip_segment_batch": (i, [vp, vp, u32, u32, i, u32, i, vp, u32, vp, vp]),
+    "e2sar_hip_reas_create": (i, [vp, C.POINTER(ReasConfig), C.POINTER(vp)]),
+    "e2sar_hip_reas_destroy": (None, [vp]),
+    "e2sar_hip_reas_arena": (vp, [vp]),
+    "e2sar_hip_reassemble_batch": (i, [vp, vp, u32, vp, u32, u64, vp]),
+    "e2sar_hip_reas_gc": (i, [vp, u64, u64, vp]),
+    "e2sar_hip_reas_poll": (i, [vp, C.POINTER(EventRec), u32, C.POINTER(u32)]),
+    "e2sar_hip_reas_lost_poll": (i, [vp, C.POINTER(LostRec), u32, C.POINTER(u32)]),
+    "e2sar_hip_reas_get_stats": (i, [vp, C.POINTER(ReasStats)]),
+    "e2sar_hip_reas_recycle": (i, [vp, i, vp]),
+    "e2sar_hip_reas_reset_stats": (i, [vp, vp]),
+}
+
+
+class E2SARHipError(RuntimeError):
+    """A failing C-ABI call: ``code`` is -(E2SARErrorc)."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"E2SAR HIP error {code}: {msg}")
+        self.code = code
+        self.msg = msg
+
+
+_lib = None
+
+
+def lib() -> C.CDLL:
+    """Load (once) and return the HIP SAR library; raises if it is not built."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise ImportError(
+                f"{LIB_PATH} is missing: build it with `make` (or __graft_entry__.build()). "
+                "The E2SAR SAR path has no CPU fallback.")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(rc: int) -> int:
+    if rc < 0:
+        raise E2SARHipError(rc, lib().e2sar_hip_last_error().decode(errors="replace"))
+    return rc

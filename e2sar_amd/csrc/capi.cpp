@@ -1,0 +1,443 @@
+// capi.cpp -- the extern "C" boundary declared in include/e2sar_hip.h.
+//
+// Host-side glue only: argument checks (mirroring the reference's sanity checks),
+// device allocation of the reassembly state, and the hand-off of device records to
+// the caller.  Every byte of event or datagram data is moved by the kernels in
+// sar_kernels.hip; there is no CPU fallback.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "e2sar_hip.h"
+#include "sar_kernels.hpp"
+
+using namespace e2sar_amd;
+
+namespace {
+
+thread_local std::string g_lastError;
+
+int fail(int code, const std::string &msg)
+{
+    g_lastError = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char *what)
+{
+    return fail(E2SAR_HIP_ERR_SYSTEM, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+#define HIP_TRY(expr)                                   \
+    do {                                                \
+        hipError_t _e = (expr);                         \
+        if (_e != hipSuccess) return hip_fail(_e, #expr); \
+    } while (0)
+
+}  // namespace
+
+struct e2sar_hip_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    bool ownStream = false;
+};
+
+struct e2sar_hip_reas {
+    e2sar_hip_ctx *ctx = nullptr;
+    e2sar_hip_reas_config cfg{};
+    ReasDev dev{};
+    void *stateMem = nullptr;        // slots | ctl | completed | lost
+    PktInfo *info = nullptr;         // per-packet scratch
+    uint32_t infoCap = 0;
+    std::mutex mu;
+};
+
+extern "C" {
+
+int e2sar_hip_abi_version(void) { return E2SAR_HIP_ABI_VERSION; }
+
+const char *e2sar_hip_last_error(void) { return g_lastError.c_str(); }
+
+int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out)
+{
+    if (!out) return fail(E2SAR_HIP_ERR_PARAMETER, "out is NULL");
+    int n = 0;
+    HIP_TRY(hipGetDeviceCount(&n));
+    if (device < 0 || device >= n) return fail(E2SAR_HIP_ERR_PARAMETER, "no such device");
+    HIP_TRY(hipSetDevice(device));
+    auto *c = new e2sar_hip_ctx;
+    c->device = device;
+    if (stream) {
+        c->stream = static_cast<hipStream_t>(stream);
+    } else {
+        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+        if (e != hipSuccess) {
+            delete c;
+            return hip_fail(e, "hipStreamCreateWithFlags");
+        }
+        c->ownStream = true;
+    }
+    *out = c;
+    return E2SAR_HIP_OK;
+}
+
+void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx)
+{
+    if (!ctx) return;
+    if (ctx->ownStream) {
+        (void)hipSetDevice(ctx->device);
+        (void)hipStreamSynchronize(ctx->stream);
+        (void)hipStreamDestroy(ctx->stream);
+    }
+    delete ctx;
+}
+
+void *e2sar_hip_ctx_stream(e2sar_hip_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
+int e2sar_hip_ctx_device(e2sar_hip_ctx *ctx) { return ctx ? ctx->device : -1; }
+
+int e2sar_hip_ctx_sync(e2sar_hip_ctx *ctx)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_device_alloc(e2sar_hip_ctx *ctx, size_t bytes, void **out)
+{
+    if (!ctx || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+    if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_device_free(e2sar_hip_ctx *ctx, void *p)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipFree(p));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_host_alloc(size_t bytes, void **out)
+{
+    if (!out) return fail(E2SAR_HIP_ERR_PARAMETER, "out is NULL");
+    hipError_t e = hipHostMalloc(out, bytes ? bytes : 1, hipHostMallocDefault);
+    if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipHostMalloc: ") + hipGetErrorString(e));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_host_free(void *p)
+{
+    HIP_TRY(hipHostFree(p));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_memcpy_h2d(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_memcpy_d2h(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+    HIP_TRY(hipStreamSynchronize(ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipMemsetAsync(dst, value, bytes, ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
+/* ---------------- geometry ---------------- */
+
+size_t e2sar_hip_total_hdr_len(int useIPv6)
+{
+    return (useIPv6 ? 40u : 20u) + 8u + E2SAR_HIP_LB_HDR_LEN + E2SAR_HIP_RE_HDR_LEN;
+}
+
+size_t e2sar_hip_max_pld_len(uint32_t mtu, int useIPv6)
+{
+    const size_t h = e2sar_hip_total_hdr_len(useIPv6);
+    return mtu > h ? mtu - h : 0;
+}
+
+size_t e2sar_hip_num_packets(size_t bytes, size_t maxPldLen)
+{
+    return maxPldLen ? (bytes + maxPldLen - 1) / maxPldLen : 0;
+}
+
+uint32_t e2sar_hip_packet_stride(size_t maxPldLen)
+{
+    return (uint32_t)((E2SAR_HIP_LBRE_HDR_LEN + maxPldLen + 15) & ~(size_t)15);
+}
+
+/* ---------------- segmentation ---------------- */
+
+int e2sar_hip_seg_plan(e2sar_hip_seg_event *events, uint32_t nEvents, size_t maxPldLen,
+                       uint32_t *totalPackets, uint32_t *maxPacketsPerEvent)
+{
+    if (!events && nEvents) return fail(E2SAR_HIP_ERR_PARAMETER, "events is NULL");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    uint64_t total = 0;
+    uint32_t mx = 0;
+    for (uint32_t i = 0; i < nEvents; i++) {
+        const uint64_t n = e2sar_hip_num_packets(events[i].bytes, maxPldLen);
+        events[i].pktBase = (uint32_t)total;
+        total += n;
+        mx = std::max<uint32_t>(mx, (uint32_t)n);
+        if (total > 0xFFFFFFFFull) return fail(E2SAR_HIP_ERR_OUT_OF_RANGE, "batch exceeds 2^32 packets");
+    }
+    if (totalPackets) *totalPackets = (uint32_t)total;
+    if (maxPacketsPerEvent) *maxPacketsPerEvent = mx;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_segment_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events,
+                            uint32_t nEvents, uint32_t maxPacketsPerEvent, int lbHdrVersion,
+                            uint32_t maxPldLen, int eventsDwordAligned, uint8_t *d_packets,
+                            uint32_t stride, uint32_t *d_lens, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (nEvents == 0) return E2SAR_HIP_OK;
+    if (!d_events || !d_packets) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    if (maxPldLen > 65535u) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen above a UDP datagram");
+    if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    const bool a4 = eventsDwordAligned && (maxPldLen % 4u == 0);
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = launch_segment(d_events, nEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen, a4,
+                                  d_packets, stride, d_lens, s);
+    if (e != hipSuccess) return hip_fail(e, "seg_kernel launch");
+    return E2SAR_HIP_OK;
+}
+
+/* ---------------- reassembly ---------------- */
+
+int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, e2sar_hip_reas **out)
+{
+    if (!ctx || !cfg || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    const uint32_t T = cfg->tableSlots;
+    if (T < 64 || (T & (T - 1))) return fail(E2SAR_HIP_ERR_PARAMETER, "tableSlots must be a power of two >= 64");
+    if (cfg->queueCapacity == 0 || cfg->lostCapacity == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "zero capacity");
+    HIP_TRY(hipSetDevice(ctx->device));
+    auto *r = new e2sar_hip_reas;
+    r->ctx = ctx;
+    r->cfg = *cfg;
+    const size_t slotsB = sizeof(ReasSlot) * (size_t)T;
+    const size_t ctlB = sizeof(ReasCtl);
+    const size_t compB = sizeof(e2sar_hip_event_rec) * (size_t)cfg->queueCapacity;
+    const size_t lostB = sizeof(e2sar_hip_lost_rec) * (size_t)cfg->lostCapacity;
+    const size_t total = slotsB + ctlB + compB + lostB;
+    hipError_t e = hipMalloc(&r->stateMem, total);
+    if (e != hipSuccess) {
+        delete r;
+        return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(state): ") + hipGetErrorString(e));
+    }
+    e = hipMalloc(reinterpret_cast<void **>(&r->dev.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
+    if (e != hipSuccess) {
+        (void)hipFree(r->stateMem);
+        delete r;
+        return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(arena): ") + hipGetErrorString(e));
+    }
+    auto *base = static_cast<uint8_t *>(r->stateMem);
+    r->dev.slots = reinterpret_cast<ReasSlot *>(base);
+    r->dev.ctl = reinterpret_cast<ReasCtl *>(base + slotsB);
+    r->dev.completed = reinterpret_cast<e2sar_hip_event_rec *>(base + slotsB + ctlB);
+    r->dev.lost = reinterpret_cast<e2sar_hip_lost_rec *>(base + slotsB + ctlB + compB);
+    r->dev.arenaBytes = cfg->arenaBytes;
+    r->dev.tableSlots = T;
+    r->dev.queueCapacity = cfg->queueCapacity;
+    r->dev.lostCapacity = cfg->lostCapacity;
+    r->dev.withLB = cfg->withLBHeader ? 1 : 0;
+    e = hipMemsetAsync(r->stateMem, 0, total, ctx->stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
+    if (e != hipSuccess) {
+        (void)hipFree(r->stateMem);
+        (void)hipFree(r->dev.arena);
+        delete r;
+        return hip_fail(e, "state init");
+    }
+    *out = r;
+    return E2SAR_HIP_OK;
+}
+
+void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
+{
+    if (!r) return;
+    (void)hipSetDevice(r->ctx->device);
+    (void)hipStreamSynchronize(r->ctx->stream);
+    (void)hipFree(r->info);
+    (void)hipFree(r->dev.arena);
+    (void)hipFree(r->stateMem);
+    delete r;
+}
+
+uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r) { return r ? r->dev.arena : nullptr; }
+
+int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                               const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (nPackets == 0) return E2SAR_HIP_OK;
+    if (!d_packets || !d_lens) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    const uint32_t hl = r->cfg.withLBHeader ? E2SAR_HIP_LBRE_HDR_LEN : E2SAR_HIP_RE_HDR_LEN;
+    if ((stride & 15u) || stride < hl + 16u) return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and > header + 16");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    if ((uint64_t)nPackets * (stride >> 4) > 0xFFFFFFFFull) return fail(E2SAR_HIP_ERR_OUT_OF_RANGE, "batch too large");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    if (nPackets > r->infoCap) {
+        if (r->info) {
+            HIP_TRY(hipStreamSynchronize(s));
+            HIP_TRY(hipFree(r->info));
+            r->info = nullptr;
+        }
+        const uint32_t cap = std::max<uint32_t>(nPackets, 4096u);
+        hipError_t e = hipMalloc(reinterpret_cast<void **>(&r->info), sizeof(PktInfo) * (size_t)cap);
+        if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(info): ") + hipGetErrorString(e));
+        r->infoCap = cap;
+    }
+    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->info, s);
+    if (e != hipSuccess) return hip_fail(e, "reassembly launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_gc(r->dev, now_ms, timeout_ms, s);
+    if (e != hipSuccess) return hip_fail(e, "gc launch");
+    return E2SAR_HIP_OK;
+}
+
+static int read_ctl(e2sar_hip_reas *r, ReasCtl &c)
+{
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    HIP_TRY(hipStreamSynchronize(r->ctx->stream));
+    HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t cap, uint32_t *nOut)
+{
+    if (!r || !nOut || (!out && cap)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    ReasCtl c;
+    int rc = read_ctl(r, c);
+    if (rc) return rc;
+    const uint32_t avail = std::min(c.nCompleted, r->dev.queueCapacity);
+    const uint32_t n = std::min(avail, cap);
+    if (n) HIP_TRY(hipMemcpy(out, r->dev.completed, sizeof(e2sar_hip_event_rec) * n, hipMemcpyDeviceToHost));
+    if (n < avail) {
+        // keep the tail queued: slide it to the front
+        HIP_TRY(hipMemcpy(r->dev.completed, r->dev.completed + n, sizeof(e2sar_hip_event_rec) * (avail - n),
+                          hipMemcpyDeviceToDevice));
+    }
+    const uint32_t left = avail - n;
+    HIP_TRY(hipMemcpy(&r->dev.ctl->nCompleted, &left, sizeof(uint32_t), hipMemcpyHostToDevice));
+    *nOut = n;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_lost_poll(e2sar_hip_reas *r, e2sar_hip_lost_rec *out, uint32_t cap, uint32_t *nOut)
+{
+    if (!r || !nOut || (!out && cap)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    ReasCtl c;
+    int rc = read_ctl(r, c);
+    if (rc) return rc;
+    const uint32_t avail = std::min(c.nLost, r->dev.lostCapacity);
+    const uint32_t n = std::min(avail, cap);
+    if (n) HIP_TRY(hipMemcpy(out, r->dev.lost, sizeof(e2sar_hip_lost_rec) * n, hipMemcpyDeviceToHost));
+    if (n < avail)
+        HIP_TRY(hipMemcpy(r->dev.lost, r->dev.lost + n, sizeof(e2sar_hip_lost_rec) * (avail - n),
+                          hipMemcpyDeviceToDevice));
+    const uint32_t left = avail - n;
+    HIP_TRY(hipMemcpy(&r->dev.ctl->nLost, &left, sizeof(uint32_t), hipMemcpyHostToDevice));
+    *nOut = n;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out)
+{
+    if (!r || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    ReasCtl c;
+    int rc = read_ctl(r, c);
+    if (rc) return rc;
+    out->enqueueLoss = c.enqueueLoss;
+    out->reassemblyLoss = c.reassemblyLoss;
+    out->eventSuccess = c.eventSuccess;
+    out->totalPackets = c.totalPackets;
+    out->totalBytes = c.totalBytes;
+    out->badHeaderDiscards = c.badHeaderDiscards;
+    out->dataErrCnt = c.dataErrCnt;
+    out->inProgress = c.inProgress;
+    out->completedPending = std::min(c.nCompleted, r->dev.queueCapacity);
+    out->lostPending = std::min(c.nLost, r->dev.lostCapacity);
+    out->arenaUsed = c.arenaTop;
+    out->tableUsed = c.tableUsed;
+    out->errorFlags = c.errorFlags;
+    out->reserved = 0;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    if (!force) {
+        ReasCtl c;
+        HIP_TRY(hipStreamSynchronize(s));
+        HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+        if (c.inProgress != 0) return fail(E2SAR_HIP_ERR_LOGIC, "events still in progress");
+        if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
+    }
+    hipError_t e = launch_recycle(r->dev, force != 0, s);
+    if (e != hipSuccess) return hip_fail(e, "recycle launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    // counters live between arenaTop and inProgress; list counts after it
+    auto *ctl = reinterpret_cast<uint8_t *>(r->dev.ctl);
+    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, totalPackets), 0,
+                           offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, totalPackets), s));
+    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, nCompleted), 0, 2 * sizeof(uint32_t), s));
+    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, errorFlags), 0, sizeof(uint32_t), s));
+    return E2SAR_HIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,79 @@
+// sar_kernels.hpp -- device data layout and launchers of the gfx950 SAR path.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "e2sar_hip.h"
+
+namespace e2sar_amd {
+
+// In-progress event table entry (the device form of eventsInProgress's
+// shared_ptr<EventQueueItem>, e2sarDPReassembler.hpp:61-99, 224-233).  64 bytes.
+struct ReasSlot {
+    uint32_t state;      // EMPTY / BUSY / READY / DONE / LOST
+    uint32_t dataId;
+    uint32_t bytes;      // bufferLength of the packet that created the event
+    uint32_t pad0;
+    uint64_t eventNum;
+    unsigned long long acc;  // curBytes (low 36 bits) | numFragments (high 28 bits)
+    uint64_t bufOff;     // arena offset of the event buffer
+    uint64_t created;    // firstSegment, caller clock in ms
+    uint64_t pad1[2];
+};
+static_assert(sizeof(ReasSlot) == 64, "slot is one 64-byte line");
+
+constexpr uint32_t kAccFragShift = 36;
+constexpr uint64_t kAccBytesMask = (1ull << kAccFragShift) - 1ull;
+
+// Counters (Reassembler::AtomicStats, e2sarDPReassembler.hpp:102-122) + allocator state.
+struct ReasCtl {
+    unsigned long long arenaTop;
+    unsigned long long totalPackets;
+    unsigned long long totalBytes;
+    unsigned long long badHeaderDiscards;
+    unsigned long long dataErrCnt;
+    unsigned long long eventSuccess;
+    unsigned long long enqueueLoss;
+    unsigned long long reassemblyLoss;
+    long long inProgress;
+    uint32_t nCompleted;
+    uint32_t nLost;
+    uint32_t tableUsed;
+    uint32_t errorFlags;
+    uint64_t pad[4];
+};
+
+// Everything a reassembly kernel needs, passed by value.
+struct ReasDev {
+    ReasSlot *slots;
+    ReasCtl *ctl;
+    e2sar_hip_event_rec *completed;
+    e2sar_hip_lost_rec *lost;
+    uint8_t *arena;
+    uint64_t arenaBytes;
+    uint32_t tableSlots;      // power of two
+    uint32_t queueCapacity;
+    uint32_t lostCapacity;
+    int withLB;
+};
+
+// Per-datagram result of classification, consumed by the scatter kernel.
+struct PktInfo {
+    uint64_t dst;     // device address of the payload's destination (0 = drop)
+    uint32_t plen;    // payload bytes
+    uint32_t hl;      // header bytes in front of the payload (36 with LB header, else 20)
+};
+static_assert(sizeof(PktInfo) == 16, "one dwordx4 per packet");
+
+hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
+                          uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
+                          bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
+                          hipStream_t stream);
+hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
+                             const uint32_t *lens, uint32_t n, uint64_t now, PktInfo *info,
+                             hipStream_t stream);
+hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);
+hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stream);
+
+}  // namespace e2sar_amd

@@ -1,0 +1,249 @@
+"""Device-level SAR API over the C ABI (``include/e2sar_hip.h``).
+
+``DeviceSegmenter`` and ``DeviceReassembler`` are thin, allocation-aware wrappers: event
+bytes, datagrams and reassembled events stay in HBM; torch is used only as the device
+memory / stream plumbing.  The reference-shaped ``Segmenter``/``Reassembler`` classes
+(``e2sar_amd.dataplane``) are built on top of these.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import _capi
+from ._capi import check, lib
+
+
+def _stream_handle(stream: Optional[torch.cuda.Stream]) -> int:
+    if stream is None:
+        stream = torch.cuda.current_stream()
+    return int(stream.cuda_stream)
+
+
+def total_hdr_len(use_ipv6: bool = False) -> int:
+    """IP + UDP + LB + RE header bytes (e2sarHeaders.hpp:419-421): 64 / 84."""
+    return int(lib().e2sar_hip_total_hdr_len(1 if use_ipv6 else 0))
+
+
+def max_pld_len(mtu: int, use_ipv6: bool = False) -> int:
+    """Segmenter maxPldLen = mtu - total header (e2sarDPSegmenter.hpp:241)."""
+    return int(lib().e2sar_hip_max_pld_len(mtu, 1 if use_ipv6 else 0))
+
+
+def num_packets(nbytes: int, max_pld: int) -> int:
+    """ceil(bytes / maxPldLen) (e2sarDPSegmenter.cpp:670)."""
+    return int(lib().e2sar_hip_num_packets(nbytes, max_pld))
+
+
+def packet_stride(max_pld: int) -> int:
+    return int(lib().e2sar_hip_packet_stride(max_pld))
+
+
+class Context:
+    """A device + stream binding (e2sar_hip_ctx)."""
+
+    def __init__(self, device: int = 0, stream: Optional[torch.cuda.Stream] = None):
+        torch.cuda.set_device(device)
+        self.device = device
+        self.torch_device = torch.device("cuda", device)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(device)
+        h = C.c_void_p()
+        check(lib().e2sar_hip_ctx_create(device, C.c_void_p(int(self.stream.cuda_stream)), C.byref(h)))
+        self._h = h
+
+    @property
+    def handle(self) -> C.c_void_p:
+        return self._h
+
+    def sync(self) -> None:
+        check(lib().e2sar_hip_ctx_sync(self._h))
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().e2sar_hip_ctx_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+@dataclass
+class SegPlan:
+    """Host event table + its device copy for one segment batch."""
+    host: "C.Array"
+    device: torch.Tensor          # uint8 tensor holding the e2sar_hip_seg_event table
+    n_events: int
+    total_packets: int
+    max_packets_per_event: int
+    aligned4: bool
+
+
+class DeviceSegmenter:
+    """Segments batches of device-resident events into device-resident datagrams.
+
+    Replaces SendThreadState::_send's fragment loop (e2sarDPSegmenter.cpp:660-871):
+    every datagram is [LB header][RE header][payload slice] exactly as the reference
+    emits it; the socket send is the caller's business (or the datagrams stay in HBM).
+    """
+
+    def __init__(self, ctx: Context, mtu: int = 1500, use_ipv6: bool = False, lb_hdr_version: int = 2):
+        self.ctx = ctx
+        self.mtu = mtu
+        self.max_pld = max_pld_len(mtu, use_ipv6)
+        if mtu > 9000:
+            raise ValueError("MTU set too long, limit 9000")       # hpp:310-311
+        if self.max_pld == 0:
+            raise ValueError("Insufficient MTU length to accommodate headers")  # hpp:315-316
+        self.stride = packet_stride(self.max_pld)
+        self.lb_hdr_version = lb_hdr_version
+
+    def plan(self, events: Sequence[tuple]) -> SegPlan:
+        """events: (data_ptr, nbytes, eventNum, dataId, entropy, lbTick) tuples, data on device."""
+        n = len(events)
+        arr = (_capi.SegEvent * max(n, 1))()
+        aligned4 = True
+        for k, (ptr, nbytes, evn, did, ent, tick) in enumerate(events):
+            if nbytes >= 1 << 32:
+                raise ValueError("event larger than 4 GiB (REHdr bufferLength is u32)")
+            e = arr[k]
+            e.data = int(ptr)
+            e.bytes = int(nbytes)
+            e.eventNum = int(evn) & (2**64 - 1)
+            e.dataId = int(did) & 0xFFFF
+            e.entropy = int(ent) & 0xFFFF
+            e.lbTick = int(tick) & (2**64 - 1)
+            aligned4 = aligned4 and (int(ptr) % 4 == 0)
+        tot = C.c_uint32()
+        mx = C.c_uint32()
+        check(lib().e2sar_hip_seg_plan(arr, n, self.max_pld, C.byref(tot), C.byref(mx)))
+        raw = np.frombuffer(bytes(arr)[: n * C.sizeof(_capi.SegEvent)], dtype=np.uint8).copy()
+        dev = torch.from_numpy(raw).to(self.ctx.torch_device, non_blocking=False)
+        return SegPlan(arr, dev, n, int(tot.value), int(mx.value), aligned4)
+
+    def alloc_packets(self, n_packets: int):
+        pk = torch.empty(max(n_packets, 1) * self.stride, dtype=torch.uint8, device=self.ctx.torch_device)
+        ln = torch.empty(max(n_packets, 1), dtype=torch.int32, device=self.ctx.torch_device)
+        return pk, ln
+
+    def segment(self, plan: SegPlan, packets: torch.Tensor, lens: Optional[torch.Tensor],
+                stream: Optional[torch.cuda.Stream] = None) -> int:
+        if packets.numel() < plan.total_packets * self.stride:
+            raise ValueError("packet buffer too small")
+        check(lib().e2sar_hip_segment_batch(
+            self.ctx.handle, C.c_void_p(plan.device.data_ptr()), plan.n_events,
+            plan.max_packets_per_event, self.lb_hdr_version, self.max_pld,
+            1 if plan.aligned4 else 0, C.c_void_p(packets.data_ptr()), self.stride,
+            C.c_void_p(lens.data_ptr() if lens is not None else 0),
+            C.c_void_p(_stream_handle(stream))))
+        return plan.total_packets
+
+
+class DeviceReassembler:
+    """Reassembles device-resident datagram batches into a device event arena.
+
+    Replaces the per-packet body of RecvThreadState::_threadBody
+    (e2sarDPReassembler.cpp:310-428), the eventsInProgress map and the event queue.
+    """
+
+    def __init__(self, ctx: Context, with_lb_header: bool = False, table_slots: int = 4096,
+                 queue_capacity: int = 4096, lost_capacity: int = 4096, arena_bytes: int = 1 << 30):
+        self.ctx = ctx
+        cfg = _capi.ReasConfig(1 if with_lb_header else 0, table_slots, queue_capacity,
+                               lost_capacity, arena_bytes)
+        h = C.c_void_p()
+        check(lib().e2sar_hip_reas_create(ctx.handle, C.byref(cfg), C.byref(h)))
+        self._h = h
+        self.with_lb_header = with_lb_header
+        self.arena_bytes = arena_bytes
+        self.arena_ptr = int(lib().e2sar_hip_reas_arena(h) or 0)
+        self._evbuf = (_capi.EventRec * queue_capacity)()
+        self._lostbuf = (_capi.LostRec * lost_capacity)()
+
+    @property
+    def handle(self):
+        return self._h
+
+    def reassemble(self, packets: torch.Tensor, stride: int, lens: torch.Tensor, n: int,
+                   now_ms: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:
+        if n == 0:
+            return
+        if lens.numel() < n or packets.numel() < n * stride:
+            raise ValueError("packet batch buffers too small")
+        check(lib().e2sar_hip_reassemble_batch(
+            self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
+            int(now_ms), C.c_void_p(_stream_handle(stream))))
+
+    def gc(self, now_ms: int, timeout_ms: int, stream: Optional[torch.cuda.Stream] = None) -> None:
+        check(lib().e2sar_hip_reas_gc(self._h, int(now_ms), int(timeout_ms), C.c_void_p(_stream_handle(stream))))
+
+    def poll(self) -> List[_capi.EventRec]:
+        n = C.c_uint32()
+        check(lib().e2sar_hip_reas_poll(self._h, self._evbuf, len(self._evbuf), C.byref(n)))
+        out = []
+        for k in range(n.value):
+            r = _capi.EventRec()
+            C.memmove(C.byref(r), C.byref(self._evbuf[k]), C.sizeof(r))
+            out.append(r)
+        return out
+
+    def lost_poll(self) -> List[_capi.LostRec]:
+        n = C.c_uint32()
+        check(lib().e2sar_hip_reas_lost_poll(self._h, self._lostbuf, len(self._lostbuf), C.byref(n)))
+        out = []
+        for k in range(n.value):
+            r = _capi.LostRec()
+            C.memmove(C.byref(r), C.byref(self._lostbuf[k]), C.sizeof(r))
+            out.append(r)
+        return out
+
+    def stats(self) -> _capi.ReasStats:
+        s = _capi.ReasStats()
+        check(lib().e2sar_hip_reas_get_stats(self._h, C.byref(s)))
+        return s
+
+    def recycle(self, force: bool = False, stream: Optional[torch.cuda.Stream] = None) -> None:
+        check(lib().e2sar_hip_reas_recycle(self._h, 1 if force else 0, C.c_void_p(_stream_handle(stream))))
+
+    def reset_stats(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        check(lib().e2sar_hip_reas_reset_stats(self._h, C.c_void_p(_stream_handle(stream))))
+
+    def event_bytes(self, rec: _capi.EventRec) -> bytes:
+        """Copy one reassembled event to host memory."""
+        buf = (C.c_uint8 * max(rec.bytes, 1))()
+        if rec.bytes:
+            check(lib().e2sar_hip_memcpy_d2h(self.ctx.handle, buf, C.c_void_p(self.arena_ptr + rec.arenaOffset),
+                                             rec.bytes))
+        return bytes(buf)[: rec.bytes]
+
+    def arena_tensor(self) -> torch.Tensor:
+        """Zero-copy uint8 view of the whole device arena."""
+        return _device_view(self.arena_ptr, self.arena_bytes, self.ctx.torch_device)
+
+    def close(self) -> None:
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().e2sar_hip_reas_destroy(self._h)
+            self._h = C.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class _CudaArray:
+    def __init__(self, ptr: int, nbytes: int):
+        self.__cuda_array_interface__ = {
+            "shape": (nbytes,), "typestr": "|u1", "data": (ptr, False), "version": 2, "strides": None,
+        }
+
+
+def _device_view(ptr: int, nbytes: int, device: torch.device) -> torch.Tensor:
+    return torch.as_tensor(_CudaArray(ptr, nbytes), device=device)

@@ -1,0 +1,208 @@
+/*
+ * e2sar_hip.h -- C ABI of the MI355X (gfx950) SAR data path.
+ *
+ * This is the drop-in boundary for the reference's segmentation / reassembly hot path
+ * (JeffersonLab/E2SAR v0.3.2).  Plain C: pointers, sizes, integer status codes; no HIP,
+ * torch or C++ types cross it.  Device pointers are passed as ordinary pointers that
+ * were allocated on the context's device (hipMalloc, torch, or e2sar_hip_device_alloc).
+ *
+ * Each entry point names the reference interface it replaces (file:line).
+ *
+ * Status codes: 0 = success, negative = -(E2SARErrorc) from include/e2sarError.hpp:23-39
+ * (e.g. -3 ParameterError, -5 OutOfRange, -7 NotFound, -10 MemoryError, -11 LogicError,
+ * -12 SystemError for a HIP runtime failure, -13 DataError).  No C++ exception crosses
+ * this boundary (the reference methods are noexcept, e2sarDPSegmenter.hpp:458-483).
+ */
+#ifndef E2SAR_HIP_H
+#define E2SAR_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define E2SAR_HIP_ABI_VERSION 1
+
+enum {
+    E2SAR_HIP_OK = 0,
+    E2SAR_HIP_ERR_PARAMETER = -3,   /* E2SARErrorc::ParameterError */
+    E2SAR_HIP_ERR_OUT_OF_RANGE = -5,/* E2SARErrorc::OutOfRange */
+    E2SAR_HIP_ERR_NOT_FOUND = -7,   /* E2SARErrorc::NotFound */
+    E2SAR_HIP_ERR_MEMORY = -10,     /* E2SARErrorc::MemoryError */
+    E2SAR_HIP_ERR_LOGIC = -11,      /* E2SARErrorc::LogicError */
+    E2SAR_HIP_ERR_SYSTEM = -12,     /* E2SARErrorc::SystemError (HIP runtime failure) */
+    E2SAR_HIP_ERR_DATA = -13        /* E2SARErrorc::DataError */
+};
+
+/* LB+RE header geometry on the wire (e2sarHeaders.hpp:302-315): 16-byte LB + 20-byte RE */
+#define E2SAR_HIP_LB_HDR_LEN 16
+#define E2SAR_HIP_RE_HDR_LEN 20
+#define E2SAR_HIP_LBRE_HDR_LEN 36
+
+/* ------------------------------------------------------------------ */
+/* library / context                                                   */
+
+int e2sar_hip_abi_version(void);
+/* Human-readable message for the last failing call on this thread (E2SARErrorInfo::msg). */
+const char *e2sar_hip_last_error(void);
+
+typedef struct e2sar_hip_ctx e2sar_hip_ctx;
+/* Bind a device.  `stream` is a hipStream_t (NULL = the context creates its own
+ * non-blocking stream).  Replaces the per-Segmenter/Reassembler thread state
+ * (e2sarDPSegmenter.hpp:213-260, e2sarDPReassembler.hpp:206-240). */
+int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out);
+void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx);
+void *e2sar_hip_ctx_stream(e2sar_hip_ctx *ctx);
+int e2sar_hip_ctx_device(e2sar_hip_ctx *ctx);
+int e2sar_hip_ctx_sync(e2sar_hip_ctx *ctx);
+
+/* memory plumbing so callers without a HIP toolchain (cgo/ctypes/C++) can drive the path */
+int e2sar_hip_device_alloc(e2sar_hip_ctx *ctx, size_t bytes, void **out);
+int e2sar_hip_device_free(e2sar_hip_ctx *ctx, void *p);
+int e2sar_hip_host_alloc(size_t bytes, void **out);           /* pinned host memory */
+int e2sar_hip_host_free(void *p);
+int e2sar_hip_memcpy_h2d(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
+int e2sar_hip_memcpy_d2h(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
+int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes);
+
+/* ------------------------------------------------------------------ */
+/* geometry (e2sarHeaders.hpp:415-421, e2sarDPSegmenter.hpp:241, e2sarDPSegmenter.cpp:670) */
+
+size_t e2sar_hip_total_hdr_len(int useIPv6);                 /* 64 (v4) / 84 (v6) */
+size_t e2sar_hip_max_pld_len(uint32_t mtu, int useIPv6);     /* mtu - total_hdr_len; 0 if mtu too small */
+size_t e2sar_hip_num_packets(size_t bytes, size_t maxPldLen);/* ceil(bytes / maxPldLen) */
+/* device packet slot: 36 + maxPldLen rounded up to 16 bytes */
+uint32_t e2sar_hip_packet_stride(size_t maxPldLen);
+
+/* ------------------------------------------------------------------ */
+/* segmentation: replaces SendThreadState::_send's fragment loop        */
+/* (e2sarDPSegmenter.cpp:660-871) for a batch of events                 */
+
+/* One event: the arguments of _send (cpp:660-662) after the host has applied the
+ * event-numbering rule (cpp:901-917 / 920-948), the dataId default (cpp:938), entropy
+ * "0 => random" (cpp:727-728), the LB tick (cpp:707-719) and ticksAsREEventNum
+ * (cpp:723-724).  40 bytes, 8-byte aligned. */
+typedef struct e2sar_hip_seg_event {
+    const uint8_t *data;   /* device address of the event bytes */
+    uint64_t eventNum;     /* RE eventNum */
+    uint64_t lbTick;       /* LB eventNum (v2) / tick (v3) */
+    uint32_t bytes;        /* event length; REHdr bufferLength is u32 (e2sarHeaders.hpp:26) */
+    uint32_t pktBase;      /* index of the event's first packet in the batch (set by seg_plan) */
+    uint16_t dataId;
+    uint16_t entropy;
+    uint32_t reserved;
+} e2sar_hip_seg_event;
+
+/* Host-side plan over a host copy of the event table: fills pktBase (exclusive prefix
+ * of ceil(bytes/maxPldLen)), returns the batch packet count and the largest per-event
+ * packet count.  Also reports whether every event is dword-aligned (fast path). */
+int e2sar_hip_seg_plan(e2sar_hip_seg_event *events, uint32_t nEvents, size_t maxPldLen,
+                       uint32_t *totalPackets, uint32_t *maxPacketsPerEvent);
+
+/* Segment nEvents events (descriptor table `d_events` already on the device) into
+ * datagrams [16-byte LB][20-byte RE][payload] at d_packets + p*stride, p = pktBase+k.
+ * d_lens[p] (optional) receives the datagram length 36 + payload.  lbHdrVersion 3
+ * selects LBHdrV3, any other value LBHdrV2 (e2sarHeaders.hpp:287-297).
+ * maxPacketsPerEvent: an upper bound (from seg_plan).  Asynchronous on `stream`
+ * (NULL = the context stream). */
+int e2sar_hip_segment_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events,
+                            uint32_t nEvents, uint32_t maxPacketsPerEvent,
+                            int lbHdrVersion, uint32_t maxPldLen, int eventsDwordAligned,
+                            uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
+                            void *stream);
+
+/* ------------------------------------------------------------------ */
+/* reassembly: replaces the RecvThreadState per-packet body             */
+/* (e2sarDPReassembler.cpp:310-428), eventsInProgress (hpp:224-233),    */
+/* the event queue (hpp:126-161) and the GC pass (cpp:236-291)          */
+
+typedef struct e2sar_hip_reas e2sar_hip_reas;
+
+typedef struct e2sar_hip_reas_config {
+    int withLBHeader;          /* ReassemblerFlags::withLBHeader (hpp:436) */
+    uint32_t tableSlots;       /* in-progress event table slots (power of two, >= 64) */
+    uint32_t queueCapacity;    /* completed-event records held until polled (QSIZE, hpp:126) */
+    uint32_t lostCapacity;     /* lost-event records held until polled */
+    uint64_t arenaBytes;       /* device arena that receives reassembled event bytes */
+} e2sar_hip_reas_config;
+
+/* Reassembled event handed to the caller (getEvent's out-params, cpp:626-641).
+ * The bytes live at e2sar_hip_reas_arena() + arenaOffset until the arena is recycled. */
+typedef struct e2sar_hip_event_rec {
+    uint64_t eventNum;
+    uint64_t arenaOffset;
+    uint32_t bytes;
+    uint16_t dataId;
+    uint16_t flags;
+    uint32_t numFragments;
+    uint32_t reserved;
+} e2sar_hip_event_rec;
+
+/* get_LostEvent's tuple (hpp:593-604) + which loss it was. */
+typedef struct e2sar_hip_lost_rec {
+    uint64_t eventNum;
+    uint64_t numFragments;
+    uint16_t dataId;
+    uint16_t enqueueLoss;      /* 1 = lost on enqueue (queue/arena full), 0 = reassembly (GC) */
+    uint32_t reserved;
+} e2sar_hip_lost_rec;
+
+/* Reassembler::ReportedStats (hpp:383-400) plus device-path diagnostics. */
+typedef struct e2sar_hip_reas_stats {
+    uint64_t enqueueLoss;
+    uint64_t reassemblyLoss;
+    uint64_t eventSuccess;
+    uint64_t totalPackets;
+    uint64_t totalBytes;
+    uint64_t badHeaderDiscards;
+    uint64_t dataErrCnt;
+    int64_t inProgress;
+    uint64_t completedPending;   /* records waiting in the completion list */
+    uint64_t lostPending;
+    uint64_t arenaUsed;
+    uint64_t tableUsed;          /* slots ever claimed since the last recycle */
+    uint32_t errorFlags;         /* bit0 table full, bit1 arena full, bit2 probe timeout */
+    uint32_t reserved;
+} e2sar_hip_reas_stats;
+
+int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg,
+                          e2sar_hip_reas **out);
+void e2sar_hip_reas_destroy(e2sar_hip_reas *r);
+/* device base of the event arena */
+uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
+
+/* Parse, validate, look up / create and scatter nPackets datagrams held at
+ * d_packets + p*stride with lengths d_lens[p] (the full datagram length as recvfrom
+ * returns it, cpp:321).  now_ms stamps firstSegment for new events (hpp:97).
+ * Asynchronous on `stream` (NULL = the context stream). */
+int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                               const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
+                               void *stream);
+
+/* GC pass: events whose first fragment is older than timeout_ms become lost
+ * (reassemblyLoss, cpp:252-274).  Asynchronous. */
+int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, void *stream);
+
+/* Drain completed events (synchronises the stream).  Records are returned in
+ * completion order of the device; *nOut <= cap.  Records beyond cap stay queued. */
+int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t cap,
+                        uint32_t *nOut);
+/* Drain lost-event records (synchronises). */
+int e2sar_hip_reas_lost_poll(e2sar_hip_reas *r, e2sar_hip_lost_rec *out, uint32_t cap,
+                             uint32_t *nOut);
+/* Stats snapshot (synchronises). */
+int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out);
+/* Recycle the arena and the event table.  Only legal when no event is in progress
+ * and every completed record has been polled (else E2SAR_HIP_ERR_LOGIC); the caller
+ * promises it no longer reads event bytes from the arena.  `force` drops in-progress
+ * events without logging them.  Asynchronous. */
+int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream);
+/* Zero every counter and the lost/completion lists (asynchronous). */
+int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* E2SAR_HIP_H */

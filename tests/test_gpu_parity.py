@@ -1,0 +1,336 @@
+"""GPU parity: the HIP path (through the C ABI) against the CPU oracle.
+
+Bar: bit-exact datagrams and event bytes, equal counters.  Sizes are ones the oracle
+finishes in seconds; full-size batches are checked through round-trip properties.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+SEND_STR = b"THIS IS A VERY LONG EVENT MESSAGE WE WANT TO SEND EVERY 1 SECONDS."  # reas test :36
+
+
+def _torch():
+    import torch
+    return torch
+
+
+def _rng_bytes(seed, n):
+    return np.random.default_rng(seed).integers(0, 256, n, dtype=np.uint8)
+
+
+def _dev(arr, ctx):
+    torch = _torch()
+    return torch.from_numpy(np.ascontiguousarray(arr)).to(ctx.torch_device)
+
+
+def _segment_gpu(ctx, events, mtu, ver, offsets=None):
+    """events: list of (np bytes, eventNum, dataId, entropy, tick); returns (pk[n,stride], lens[n])."""
+    torch = _torch()
+    from e2sar_amd import sar
+    seg = sar.DeviceSegmenter(ctx, mtu=mtu, lb_hdr_version=ver)
+    # pack all events in one device arena; offsets let a test misalign an event on purpose
+    offs, cur = [], 0
+    for k, (b, *_r) in enumerate(events):
+        pad = offsets[k] if offsets else 0
+        cur = (cur + 255) // 256 * 256 + pad
+        offs.append(cur)
+        cur += len(b)
+    host = np.zeros(max(cur, 1), np.uint8)
+    for (b, *_r), o in zip(events, offs):
+        host[o:o + len(b)] = b
+    darena = _dev(host, ctx)
+    base = darena.data_ptr()
+    plan = seg.plan([(base + o, len(b), e, d, en, t) for (b, e, d, en, t), o in zip(events, offs)])
+    pk, ln = seg.alloc_packets(plan.total_packets)
+    seg.segment(plan, pk, ln)
+    torch.cuda.synchronize()
+    n = plan.total_packets
+    return (pk[: n * seg.stride].view(n, seg.stride).cpu().numpy(), ln[:n].cpu().numpy().astype(np.uint32),
+            seg)
+
+
+def _segment_oracle(events, mtu, ver, stride):
+    mp = O.max_pld_len(mtu)
+    pks, lns = [], []
+    for b, e, d, en, t in events:
+        p, l = O.segment_event(np.frombuffer(bytes(b), np.uint8), e, d, en, t, ver, mp, stride)
+        pks.append(p)
+        lns.append(l)
+    if not pks:
+        return np.zeros((0, stride), np.uint8), np.zeros(0, np.uint32)
+    return np.concatenate(pks), np.concatenate(lns)
+
+
+def _assert_same_datagrams(gp, gl, op, ol):
+    assert gp.shape[0] == op.shape[0], (gp.shape, op.shape)
+    np.testing.assert_array_equal(gl, ol)
+    for k in range(len(ol)):
+        L = int(ol[k])
+        if not np.array_equal(gp[k, :L], op[k, :L]):
+            bad = np.nonzero(gp[k, :L] != op[k, :L])[0]
+            raise AssertionError(f"datagram {k} differs at bytes {bad[:16]} (len {L})")
+
+
+# ----------------------------------------------------------------------------------
+# segmentation parity
+
+
+@pytest.mark.parametrize("mtu,npk", [(80, 5), (104, 2), (1500, 1)])
+def test_seg_send_str_counts_and_bytes(hip, mtu, npk):
+    # e2sar_reas_test.cpp:195/254 (MTU 80 -> 5 pkts), e2sar_seg_test.cpp:116/174 (MTU 104 -> 2)
+    ev = [(np.frombuffer(SEND_STR, np.uint8), 0, 4321, 0xBEEF, 0x0123456789ABCDEF)]
+    gp, gl, seg = _segment_gpu(hip, ev, mtu, 2)
+    assert gp.shape[0] == npk
+    op, ol = _segment_oracle(ev, mtu, 2, seg.stride)
+    _assert_same_datagrams(gp, gl, op, ol)
+
+
+@pytest.mark.parametrize("mtu,ver,nbytes", [
+    (1500, 2, 1 << 20), (1500, 3, 1 << 20), (9000, 2, 1 << 20), (9000, 3, 8 << 20),
+    (1500, 2, 100000), (9000, 3, 3 * 8936 + 1), (1500, 3, 1436), (1500, 2, 1437)])
+def test_seg_parity_sizes(hip, mtu, ver, nbytes):
+    evs = [(_rng_bytes(7 + k, nbytes), k, 4321, 1 + (k * 0x9E37) % 65535, (1 << 48) + k) for k in range(3)]
+    gp, gl, seg = _segment_gpu(hip, evs, mtu, ver)
+    op, ol = _segment_oracle(evs, mtu, ver, seg.stride)
+    _assert_same_datagrams(gp, gl, op, ol)
+
+
+def test_seg_known_answer_headers(hip):
+    # A, v2, eventNum 0, dataId 4321, entropy 0xBEEF, tick 0x0123456789ABCDEF
+    ev = [(_rng_bytes(1, 1 << 20), 0, 4321, 0xBEEF, 0x0123456789ABCDEF)]
+    gp, gl, _ = _segment_gpu(hip, ev, 1500, 2)
+    assert gp.shape[0] == 731
+    assert gp[0, :36].tobytes().hex() == "4c4202010000beef0123456789abcdef100010e100000000001000000000000000000000"
+    assert gp[1, 16:28].tobytes().hex() == "100010e10000059c00100000"
+    assert gp[730, 16:28].tobytes().hex() == "100010e1000ffed800100000"
+    assert int(gl[730]) == 36 + 296
+    ev = [(_rng_bytes(2, 8 << 20), 7, 4321, 0xBEEF, 0x0123456789ABCDEF)]
+    gp, gl, _ = _segment_gpu(hip, ev, 9000, 3)
+    assert gp.shape[0] == 939
+    assert gp[0, :36].tobytes().hex() == "4c420301cdefbeef0123456789abcdef100010e100000000008000000000000000000007"
+    assert int(gl[938]) == 36 + 6640
+
+
+def test_seg_ragged_batch(hip):
+    sizes = [0, 1, 2, 3, 4, 5, 11, 12, 13, 15, 16, 17, 1435, 1436, 1437, 2872, 2873, 65536 + 3, 1 << 20]
+    evs = [(_rng_bytes(100 + k, s), 1000 + k, 7 + k, (k * 77) & 0xFFFF, k * 0x100000001) for k, s in enumerate(sizes)]
+    for ver in (2, 3):
+        gp, gl, seg = _segment_gpu(hip, evs, 1500, ver)
+        op, ol = _segment_oracle(evs, 1500, ver, seg.stride)
+        _assert_same_datagrams(gp, gl, op, ol)
+
+
+def test_seg_generic_paths(hip):
+    # misaligned event bases and a maxPldLen that is not a multiple of 4 take the byte path
+    sizes = [1, 5, 1437, 4099, 100003]
+    evs = [(_rng_bytes(300 + k, s), k, 1, 2, 3) for k, s in enumerate(sizes)]
+    gp, gl, seg = _segment_gpu(hip, evs, 1500, 2, offsets=[1, 2, 3, 1, 2])
+    op, ol = _segment_oracle(evs, 1500, 2, seg.stride)
+    _assert_same_datagrams(gp, gl, op, ol)
+    gp, gl, seg = _segment_gpu(hip, evs, 1499, 3)                 # maxPld 1435
+    op, ol = _segment_oracle(evs, 1499, 3, seg.stride)
+    _assert_same_datagrams(gp, gl, op, ol)
+    gp, gl, seg = _segment_gpu(hip, evs, 67, 2)                   # maxPld 3
+    op, ol = _segment_oracle(evs[:3], 67, 2, seg.stride)
+    n3 = op.shape[0]
+    _assert_same_datagrams(gp[:n3], gl[:n3], op, ol)
+
+
+# ----------------------------------------------------------------------------------
+# reassembly parity
+
+
+def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096):
+    """Reassemble datagram rows pk[n, stride] (lens ln) on the GPU; returns ({(ev,d): bytes}, stats, reas)."""
+    from e2sar_amd import sar
+    torch = _torch()
+    n, stride = pk.shape
+    st16 = (stride + 15) // 16 * 16
+    buf = np.zeros((max(n, 1), st16), np.uint8)
+    buf[:n, :stride] = pk
+    dpk = _dev(buf.reshape(-1), ctx)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), ctx)
+    R = sar.DeviceReassembler(ctx, with_lb_header=with_lb, table_slots=table, arena_bytes=arena)
+    cuts = np.linspace(0, n, batches + 1).astype(int)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if b > a:
+            R.reassemble(dpk[a * st16:], st16, dln[a:], int(b - a), now_ms=now)
+    torch.cuda.synchronize()
+    got = {}
+    for rec in R.poll():
+        key = (rec.eventNum, rec.dataId)
+        assert key not in got
+        got[key] = (R.event_bytes(rec), rec.numFragments)
+    return got, R.stats(), R
+
+
+def _reas_oracle(pk, ln, with_lb, qcap=100000):
+    r = O.Reassembler(with_lb, qcap)
+    r.push_batch(pk, ln)
+    out = {}
+    for b, e, d in r.pop_all():
+        out[(e, d)] = b
+    return out, r.stats(), r
+
+
+def _events_stream(n_ev, size, mtu, ver=2, seed=0, data_id=4321):
+    mp = O.max_pld_len(mtu)
+    stride = (36 + mp + 15) // 16 * 16
+    evs, pks, lns = [], [], []
+    for k in range(n_ev):
+        b = _rng_bytes(seed + k, size if np.isscalar(size) else size[k])
+        evs.append(b)
+        p, l = O.segment_event(b, k, data_id, 1 + k, (1 << 48) + k, ver, mp, stride)
+        pks.append(p)
+        lns.append(l)
+    return evs, np.concatenate(pks), np.concatenate(lns)
+
+
+def _check_reas(got, st, ref, rst):
+    assert set(got) == set(ref), (sorted(got)[:5], sorted(ref)[:5])
+    for k in ref:
+        assert got[k][0] == ref[k], f"event {k} bytes differ"
+    for f in ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt",
+              "enqueueLoss", "reassemblyLoss"):
+        assert getattr(st, f) == rst[f], (f, getattr(st, f), rst[f])
+    assert st.inProgress == rst["inProgress"]
+
+
+@pytest.mark.parametrize("mtu,size,n_ev", [(1500, 1 << 20, 8), (9000, 1 << 20, 8), (80, 67, 5),
+                                           (1500, [1, 1436, 1437, 5000, 100000, 3], 6)])
+def test_reas_in_order_with_lb(hip, mtu, size, n_ev):
+    evs, pk, ln = _events_stream(n_ev, size, mtu)
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    got, st, _ = _reas_gpu(hip, pk, ln, True)
+    _check_reas(got, st, ref, rst)
+    for k, b in enumerate(evs):
+        assert ref[(k, 4321)] == b.tobytes()
+
+
+def test_reas_without_lb_header(hip):
+    evs, pk, ln = _events_stream(4, 50000, 1500)
+    pk2 = np.zeros_like(pk)
+    pk2[:, : pk.shape[1] - 16] = pk[:, 16:]
+    ln2 = ln - 16
+    ref, rst, _ = _reas_oracle(pk2, ln2, False)
+    got, st, _ = _reas_gpu(hip, pk2, ln2, False)
+    _check_reas(got, st, ref, rst)
+
+
+def test_reas_interleaved_offset0_first(hip):
+    # events interleaved and each event's tail fragments shuffled, offset-0 fragment first
+    evs, pk, ln = _events_stream(6, 30000, 1500, seed=11)
+    order = []
+    per = []
+    idx = 0
+    for k in range(6):
+        n = O.num_packets(30000, O.max_pld_len(1500))
+        per.append(list(range(idx, idx + n)))
+        idx += n
+    rnd = random.Random(5)
+    firsts = [p[0] for p in per]
+    rest = [i for p in per for i in p[1:]]
+    rnd.shuffle(rest)
+    order = firsts + rest
+    pk, ln = pk[order], ln[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    for batches in (1, 3):
+        got, st, _ = _reas_gpu(hip, pk, ln, True, batches=batches)
+        _check_reas(got, st, ref, rst)
+
+
+def test_reas_bad_and_short_datagrams(hip):
+    evs, pk, ln = _events_stream(5, 20000, 1500, seed=21)
+    pk = pk.copy()
+    ln = ln.copy()
+    pk[3, 16] = 0x20          # RE version 2 -> invalid
+    pk[9, 17] = 1             # reserved byte set -> invalid
+    ln[12] = 30               # shorter than LB+RE headers
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    got, st, R = _reas_gpu(hip, pk, ln, True, now=100)
+    _check_reas(got, st, ref, rst)
+    assert st.badHeaderDiscards == 3
+    # incomplete events are reported lost by GC, with their fragment counts
+    ro = O.Reassembler(True)
+    ro.set_time(100)
+    ro.push_batch(pk, ln)
+    ro.pop_all()
+    ro.set_time(1000)
+    ro.gc(500)
+    ref_lost = sorted(ro.lost_pop_all())
+    R.gc(now_ms=1000, timeout_ms=500)
+    lost = sorted((r.eventNum, r.dataId, r.numFragments) for r in R.lost_poll())
+    assert lost == ref_lost
+    s2 = R.stats()
+    assert s2.reassemblyLoss == ro.stats()["reassemblyLoss"] and s2.inProgress == 0
+
+
+def test_reas_bounds_violation_counted(hip):
+    evs, pk, ln = _events_stream(2, 5000, 1500, seed=31)
+    pk = pk.copy()
+    # rewrite fragment 1's bufferOffset so it overruns the event (reference would overflow)
+    pk[1, 20:24] = np.frombuffer((4990).to_bytes(4, "big"), np.uint8)
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    got, st, _ = _reas_gpu(hip, pk, ln, True)
+    _check_reas(got, st, ref, rst)
+    assert st.dataErrCnt == 1
+
+
+def test_reas_multiple_data_ids_same_event_numbers(hip):
+    e1, p1, l1 = _events_stream(4, 9000, 1500, seed=41, data_id=1)
+    e2, p2, l2 = _events_stream(4, 9000, 1500, seed=51, data_id=2)
+    pk = np.concatenate([p1, p2])
+    ln = np.concatenate([l1, l2])
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    got, st, _ = _reas_gpu(hip, pk, ln, True, table=64)
+    _check_reas(got, st, ref, rst)
+    assert len(got) == 8
+
+
+def test_reas_queue_and_arena_limits(hip):
+    # arena too small for all events: the overflow is an enqueue loss, never a fault
+    evs, pk, ln = _events_stream(6, 100000, 1500, seed=61)
+    got, st, R = _reas_gpu(hip, pk, ln, True, arena=3 * 100096)
+    assert st.eventSuccess == 6
+    assert len(got) == 3 and st.enqueueLoss == 3
+    assert st.errorFlags & 2
+    for (e, d), (b, nf) in got.items():
+        assert b == evs[e].tobytes()
+
+
+# ----------------------------------------------------------------------------------
+# full-size round trips (size-independent properties)
+
+
+@pytest.mark.parametrize("mtu,size,n_ev,ver", [(1500, 1 << 20, 96, 2), (9000, 8 << 20, 12, 3)])
+def test_roundtrip_full_size(hip, mtu, size, n_ev, ver):
+    torch = _torch()
+    from e2sar_amd import sar
+    g = torch.Generator(device=hip.torch_device)
+    g.manual_seed(1234)
+    src = torch.randint(0, 256, (n_ev, size), dtype=torch.uint8, device=hip.torch_device, generator=g)
+    seg = sar.DeviceSegmenter(hip, mtu=mtu, lb_hdr_version=ver)
+    plan = seg.plan([(src[k].data_ptr(), size, k, 4321, 1 + k, (1 << 48) + k) for k in range(n_ev)])
+    pk, ln = seg.alloc_packets(plan.total_packets)
+    seg.segment(plan, pk, ln)
+    R = sar.DeviceReassembler(hip, with_lb_header=True, arena_bytes=n_ev * ((size + 255) // 256 * 256) + 4096)
+    R.reassemble(pk, seg.stride, ln, plan.total_packets)
+    recs = R.poll()
+    st = R.stats()
+    assert st.eventSuccess == n_ev and len(recs) == n_ev and st.inProgress == 0
+    assert st.totalPackets == plan.total_packets == n_ev * O.num_packets(size, seg.max_pld)
+    arena = R.arena_tensor()
+    for rec in recs:
+        assert rec.numFragments == O.num_packets(size, seg.max_pld)
+        out = arena[rec.arenaOffset: rec.arenaOffset + rec.bytes]
+        assert torch.equal(out, src[rec.eventNum]), f"event {rec.eventNum} differs"
+    # recycle and go again: same results from a clean table
+    R.recycle(force=False)
+    R.reassemble(pk, seg.stride, ln, plan.total_packets)
+    assert len(R.poll()) == n_ev

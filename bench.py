@@ -1,0 +1,307 @@
+#!/usr/bin/env python3
+"""Benchmark: GiB/s of event payload segmented + reassembled, device-resident, on MI355X.
+
+One step = every event of this rank's working set (default 1024 x 1 MiB) is segmented
+into LB+RE datagrams (MTU 1500 -> 731 per event) and the datagrams are reassembled
+into a fresh event arena, batch by batch (default 64 events = 46,784 datagrams per
+batch, so each batch's datagrams stay in the 256 MiB Infinity Cache between the two
+kernels).  Inputs (event bytes + the 40-byte-per-event descriptor tables) are resident
+in HBM before timing starts.  N>1: one process per GPU (torch.distributed.run), events
+sharded by eventNum % world (weak scaling, no data-path collective).
+
+Prints ONE JSON line on rank 0.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mtu", type=int, default=1500)
+    ap.add_argument("--event-bytes", type=int, default=1 << 20)
+    ap.add_argument("--events", type=int, default=1024, help="events per rank per step")
+    ap.add_argument("--batch-events", type=int, default=64, help="events per segment/reassemble launch")
+    ap.add_argument("--lb-version", type=int, default=2)
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
+    ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
+    ap.add_argument("--roofline-steps", type=int, default=2)
+    ap.add_argument("--quiet", action="store_true")
+    return ap.parse_args()
+
+
+def log(args, *a):
+    if not args.quiet:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(args, budget_s: float):
+    """The oracle (plain-C restatement of _send + recv body) on 1 host core, on a bounded
+    sample of the same workload: segment + reassemble 16 events of event-bytes repeatedly."""
+    import numpy as np
+
+    import oracle_ffi as O
+    import sar_inputs as S
+
+    B = args.event_bytes
+    n_ev = max(1, min(16, (256 << 20) // B))
+    mp = O.max_pld_len(args.mtu)
+    stride = (36 + mp + 15) // 16 * 16
+    npk = O.num_packets(B, mp)
+    events = [S.event_bytes(i, B) for i in range(n_ev)]
+    pk = np.zeros((npk, stride), np.uint8)
+    ln = np.zeros(npk, np.uint32)
+    done_bytes = 0
+    passes = 0
+    t0 = time.perf_counter()
+    while True:
+        r = O.Reassembler(True, 1 << 20)
+        for i, ev in enumerate(events):
+            O.lib().e2o_segment_event(ev.ctypes.data, B, i, S.DATA_ID, S.entropy(i), S.lb_tick(i),
+                                      args.lb_version, mp, pk.ctypes.data, stride, ln.ctypes.data)
+            r.push_batch(pk, ln)
+            out = r.pop(B + 16)
+            assert out is not None and len(out[0]) == B
+        done_bytes += n_ev * B
+        passes += 1
+        del r
+        if time.perf_counter() - t0 >= budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": round(done_bytes / dt / 2**30, 4), "unit": "GiB/s", "cores": 1, "kind": "port",
+            "sample": f"{passes} passes x {n_ev} events x {B} B, MTU {args.mtu}: oracle segment_event "
+                      f"(header + payload memcpy per datagram) then recv body (parse, map lookup, memcpy) "
+                      f"into a fresh event, 1 thread, {dt:.1f} s"}
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+
+    from e2sar_amd import sar
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    ctx = sar.Context(local)
+
+    B = args.event_bytes
+    E = args.events
+    seg = sar.DeviceSegmenter(ctx, mtu=args.mtu, lb_hdr_version=args.lb_version)
+    mp, stride = seg.max_pld, seg.stride
+    npk = sar.num_packets(B, mp)
+
+    # ---- inputs resident in HBM: event bytes + per-batch descriptor tables ----
+    g = torch.Generator(device=dev)
+    g.manual_seed(0xE25A2 + rank)
+    ev_stride = (B + 255) // 256 * 256
+    src = torch.randint(0, 256, (E, ev_stride), dtype=torch.uint8, device=dev, generator=g)
+    evnum = lambda i: i * world + rank          # owner rank = eventNum % world
+    plans = []
+    for b0 in range(0, E, args.batch_events):
+        idx = range(b0, min(E, b0 + args.batch_events))
+        plans.append(seg.plan([(src[i].data_ptr(), B, evnum(i), 4321, 1 + (evnum(i) * 0x9E37) % 65535,
+                                (1 << 48) + evnum(i)) for i in idx]))
+    max_batch_pk = max(p.total_packets for p in plans)
+    nbuf = 2 if args.overlap else 1
+    bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
+    table = 1
+    while table < 2 * E:
+        table <<= 1
+    R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
+                              lost_capacity=1024, arena_bytes=E * ev_stride + 4096)
+    torch.cuda.synchronize()
+
+    def step():
+        """One step: recycle the event table/arena, then segment -> reassemble every batch.
+        With --overlap, reassembly of batch b runs on a second stream concurrently with
+        segmentation of batch b+1 (double-buffered datagram slots)."""
+        s0 = torch.cuda.current_stream()
+        R.recycle(force=True)
+        if not args.overlap:
+            pk, ln = bufs[0]
+            for p in plans:
+                seg.segment(p, pk, ln)
+                R.reassemble(pk, stride, ln, p.total_packets)
+            return
+        s1 = side
+        s1.wait_stream(s0)
+        done = [None] * nbuf
+        for k, p in enumerate(plans):
+            pk, ln = bufs[k % nbuf]
+            if done[k % nbuf] is not None:
+                s0.wait_event(done[k % nbuf])
+            seg.segment(p, pk, ln, stream=s0)
+            ev = torch.cuda.Event()
+            ev.record(s0)
+            s1.wait_event(ev)
+            R.reassemble(pk, stride, ln, p.total_packets, stream=s1)
+            d = torch.cuda.Event()
+            d.record(s1)
+            done[k % nbuf] = d
+        s0.wait_stream(s1)
+
+    side = torch.cuda.Stream() if args.overlap else None
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # ---- correctness gate (outside the timed region) ----
+    def verify():
+        recs = R.poll()
+        st = R.stats()
+        arena = R.arena_tensor()
+        ok = (len(recs) == E and st.inProgress == 0 and st.badHeaderDiscards == 0
+              and all(r.numFragments == npk for r in recs))
+        if ok:
+            for r in recs:
+                i = (r.eventNum - rank) // world
+                if not torch.equal(arena[r.arenaOffset: r.arenaOffset + B], src[i, :B]):
+                    ok = False
+                    break
+        if not ok:
+            raise SystemExit(f"rank {rank}: round-trip verification FAILED ({len(recs)} records, stats "
+                             f"eventSuccess={st.eventSuccess} inProgress={st.inProgress})")
+        return True
+
+    verified = None
+    if not args.no_verify:
+        step()
+        torch.cuda.synchronize()
+        verified = verify()
+
+    # ---- the step as one HIP graph (kills per-launch host overhead) ----
+    graph = None
+    if not args.eager:
+        graph = torch.cuda.CUDAGraph()
+        cap = torch.cuda.Stream()
+        cap.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(cap):
+            step()                          # warm the capture stream once
+        torch.cuda.synchronize()
+        with torch.cuda.graph(graph, stream=cap):
+            step()
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        if not args.no_verify:
+            verified = verify() and verified is not False
+
+    # ---- timed region ----
+    K = args.steps
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(K):
+        if graph is not None:
+            graph.replay()
+        else:
+            step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # ---- per-kernel durations: HIP events around each launch, serialized, same stream ----
+    stream = torch.cuda.current_stream()
+    pk, ln = bufs[0]
+    seg_ms, reas_ms = [], []
+    for _ in range(args.roofline_steps):
+        R.recycle(force=True)
+        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in plans]
+        for k, p in enumerate(plans):
+            evs[k][0].record(stream)
+            seg.segment(p, pk, ln)
+            evs[k][1].record(stream)
+            R.reassemble(pk, stride, ln, p.total_packets)
+            evs[k][2].record(stream)
+        torch.cuda.synchronize()
+        seg_ms += [e[0].elapsed_time(e[1]) for e in evs]
+        reas_ms += [e[1].elapsed_time(e[2]) for e in evs]
+    per_launch_events = sum(p.n_events for p in plans) / len(plans)
+    launch_bytes = per_launch_events * (2 * B + 36 * npk)   # seg: B + (B+36N); reas: (B+36N) + B
+    seg_avg = sum(seg_ms) / len(seg_ms)
+    reas_avg = sum(reas_ms) / len(reas_ms)
+    dom, dom_ms = ("seg_kernel", seg_avg) if seg_avg >= reas_avg else ("reas_kernel", reas_avg)
+    achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
+
+    total_payload = E * B * world * K
+    value = total_payload / elapsed / 2**30
+    step_bytes = E * (4 * B + 72 * npk)
+
+    cpu = None
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        cpu = cpu_baseline(args, args.cpu_seconds)
+
+    if rank == 0:
+        line = {
+            "metric": "GiB/s event payload segmented+reassembled, device-resident, 1/2/4/8 MI355X",
+            "value": round(value, 3),
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": K,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / K * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (torch Philox uniform bytes, seeded per rank)",
+            "config": {
+                "workload": (f"{E} x {B} B events/rank/step, MTU {args.mtu} (maxPld {mp}, {npk} datagrams/event), "
+                             f"LB v{args.lb_version} + RE headers, withLBHeader, {args.batch_events} events per "
+                             f"launch, segment -> reassemble in HBM"),
+                "events_per_rank": E, "event_bytes": B, "mtu": args.mtu, "batch_events": args.batch_events,
+                "parallelism": f"eventNum % {world} sharding (no collective)",
+                "launch": "eager" if args.eager else "hipGraph per step",
+                "overlap": bool(args.overlap),
+                "verified_roundtrip": verified,
+            },
+            "roofline": {
+                "bound": "hbm",
+                "kernel": dom,
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "avg_launch_ms": {"seg_kernel": round(seg_avg, 5), "reas_kernel": round(reas_avg, 5)},
+                "algorithmic_bytes_per_launch": int(launch_bytes),
+                "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
+            },
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -108,6 +108,8 @@ SIGNATURES = {
     "e2sar_hip_last_error": (C.c_char_p, []),
     "e2sar_hip_ctx_create": (i, [i, vp, C.POINTER(vp)]),
     "e2sar_hip_ctx_destroy": (None, [vp]),
+    "e2sar_hip_stream_create": (i, [i, C.POINTER(vp)]),
+    "e2sar_hip_stream_destroy": (i, [vp]),
     "e2sar_hip_ctx_stream": (vp, [vp]),
     "e2sar_hip_ctx_device": (i, [vp]),
     "e2sar_hip_ctx_sync": (i, [vp]),

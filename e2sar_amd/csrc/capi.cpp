@@ -45,7 +45,6 @@ int hip_fail(hipError_t e, const char *what)
 struct e2sar_hip_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
-    bool ownStream = false;
 };
 
 struct e2sar_hip_reas {
@@ -53,8 +52,6 @@ struct e2sar_hip_reas {
     e2sar_hip_reas_config cfg{};
     ReasDev dev{};
     void *stateMem = nullptr;        // slots | ctl | completed | lost
-    PktInfo *info = nullptr;         // per-packet scratch
-    uint32_t infoCap = 0;
     std::mutex mu;
 };
 
@@ -73,16 +70,7 @@ int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out)
     HIP_TRY(hipSetDevice(device));
     auto *c = new e2sar_hip_ctx;
     c->device = device;
-    if (stream) {
-        c->stream = static_cast<hipStream_t>(stream);
-    } else {
-        hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
-        if (e != hipSuccess) {
-            delete c;
-            return hip_fail(e, "hipStreamCreateWithFlags");
-        }
-        c->ownStream = true;
-    }
+    c->stream = static_cast<hipStream_t>(stream);   // NULL = the device's default stream
     *out = c;
     return E2SAR_HIP_OK;
 }
@@ -90,12 +78,26 @@ int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out)
 void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx)
 {
     if (!ctx) return;
-    if (ctx->ownStream) {
-        (void)hipSetDevice(ctx->device);
-        (void)hipStreamSynchronize(ctx->stream);
-        (void)hipStreamDestroy(ctx->stream);
-    }
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
     delete ctx;
+}
+
+int e2sar_hip_stream_create(int device, void **out)
+{
+    if (!out) return fail(E2SAR_HIP_ERR_PARAMETER, "out is NULL");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIP_TRY(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    *out = s;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_stream_destroy(void *stream)
+{
+    if (!stream) return E2SAR_HIP_OK;
+    HIP_TRY(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return E2SAR_HIP_OK;
 }
 
 void *e2sar_hip_ctx_stream(e2sar_hip_ctx *ctx) { return ctx ? ctx->stream : nullptr; }
@@ -245,7 +247,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->ctx = ctx;
     r->cfg = *cfg;
     const size_t slotsB = sizeof(ReasSlot) * (size_t)T;
-    const size_t ctlB = sizeof(ReasCtl);
+    const size_t ctlB = sizeof(ReasCtl) + sizeof(ReasShard) * kShards;
     const size_t compB = sizeof(e2sar_hip_event_rec) * (size_t)cfg->queueCapacity;
     const size_t lostB = sizeof(e2sar_hip_lost_rec) * (size_t)cfg->lostCapacity;
     const size_t total = slotsB + ctlB + compB + lostB;
@@ -263,6 +265,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     auto *base = static_cast<uint8_t *>(r->stateMem);
     r->dev.slots = reinterpret_cast<ReasSlot *>(base);
     r->dev.ctl = reinterpret_cast<ReasCtl *>(base + slotsB);
+    r->dev.shards = reinterpret_cast<ReasShard *>(base + slotsB + sizeof(ReasCtl));
     r->dev.completed = reinterpret_cast<e2sar_hip_event_rec *>(base + slotsB + ctlB);
     r->dev.lost = reinterpret_cast<e2sar_hip_lost_rec *>(base + slotsB + ctlB + compB);
     r->dev.arenaBytes = cfg->arenaBytes;
@@ -287,7 +290,6 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     if (!r) return;
     (void)hipSetDevice(r->ctx->device);
     (void)hipStreamSynchronize(r->ctx->stream);
-    (void)hipFree(r->info);
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
     delete r;
@@ -308,18 +310,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    if (nPackets > r->infoCap) {
-        if (r->info) {
-            HIP_TRY(hipStreamSynchronize(s));
-            HIP_TRY(hipFree(r->info));
-            r->info = nullptr;
-        }
-        const uint32_t cap = std::max<uint32_t>(nPackets, 4096u);
-        hipError_t e = hipMalloc(reinterpret_cast<void **>(&r->info), sizeof(PktInfo) * (size_t)cap);
-        if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(info): ") + hipGetErrorString(e));
-        r->infoCap = cap;
-    }
-    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->info, s);
+    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;
 }
@@ -335,11 +326,22 @@ int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, v
     return E2SAR_HIP_OK;
 }
 
-static int read_ctl(e2sar_hip_reas *r, ReasCtl &c)
+static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
 {
     HIP_TRY(hipSetDevice(r->ctx->device));
     HIP_TRY(hipStreamSynchronize(r->ctx->stream));
     HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+    if (sum) {
+        std::vector<ReasShard> sh(kShards);
+        HIP_TRY(hipMemcpy(sh.data(), r->dev.shards, sizeof(ReasShard) * kShards, hipMemcpyDeviceToHost));
+        *sum = ReasShard{};
+        for (const auto &x : sh) {
+            sum->totalPackets += x.totalPackets;
+            sum->totalBytes += x.totalBytes;
+            sum->badHeaderDiscards += x.badHeaderDiscards;
+            sum->dataErrCnt += x.dataErrCnt;
+        }
+    }
     return E2SAR_HIP_OK;
 }
 
@@ -388,15 +390,16 @@ int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out)
     if (!r || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
     std::lock_guard<std::mutex> lk(r->mu);
     ReasCtl c;
-    int rc = read_ctl(r, c);
+    ReasShard t;
+    int rc = read_ctl(r, c, &t);
     if (rc) return rc;
     out->enqueueLoss = c.enqueueLoss;
     out->reassemblyLoss = c.reassemblyLoss;
     out->eventSuccess = c.eventSuccess;
-    out->totalPackets = c.totalPackets;
-    out->totalBytes = c.totalBytes;
-    out->badHeaderDiscards = c.badHeaderDiscards;
-    out->dataErrCnt = c.dataErrCnt;
+    out->totalPackets = t.totalPackets;
+    out->totalBytes = t.totalBytes;
+    out->badHeaderDiscards = t.badHeaderDiscards;
+    out->dataErrCnt = t.dataErrCnt;
     out->inProgress = c.inProgress;
     out->completedPending = std::min(c.nCompleted, r->dev.queueCapacity);
     out->lostPending = std::min(c.nLost, r->dev.lostCapacity);
@@ -431,10 +434,11 @@ int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    // counters live between arenaTop and inProgress; list counts after it
+    // event counters live between arenaTop and inProgress; list counts after it
     auto *ctl = reinterpret_cast<uint8_t *>(r->dev.ctl);
-    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, totalPackets), 0,
-                           offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, totalPackets), s));
+    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, eventSuccess), 0,
+                           offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, eventSuccess), s));
+    HIP_TRY(hipMemsetAsync(r->dev.shards, 0, sizeof(ReasShard) * kShards, s));
     HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, nCompleted), 0, 2 * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, errorFlags), 0, sizeof(uint32_t), s));
     return E2SAR_HIP_OK;

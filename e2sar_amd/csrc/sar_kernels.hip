@@ -32,79 +32,114 @@ __device__ __forceinline__ void st16(uint8_t *p, u32x4 v) { *(E2SAR_GLOBAL u32x4
 __device__ __forceinline__ uint32_t ld4(const uint8_t *p) { return *(const E2SAR_GLOBAL uint32_t *)(p); }
 __device__ __forceinline__ void st4(uint8_t *p, uint32_t v) { *(E2SAR_GLOBAL uint32_t *)(p) = v; }
 __device__ __forceinline__ uint8_t ld1(const uint8_t *p) { return *(const E2SAR_GLOBAL uint8_t *)(p); }
+// Non-temporal forms for bytes touched once: event bytes read by seg_kernel, event bytes
+// written by reas_kernel.  Datagram bytes keep the default policy so a batch written by
+// seg_kernel can still be in L2 / Infinity Cache when reas_kernel reads it.
+__device__ __forceinline__ u32x4 ld16_nt(const uint8_t *p)
+{
+    return __builtin_nontemporal_load((const E2SAR_GLOBAL u32x4_a4 *)(p));
+}
+__device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4 *)(p)); }
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
 
 // ---------------------------------------------------------------------------------
 // segmentation
 
-__device__ __forceinline__ uint32_t hdr_word(const HdrWords &h, uint32_t idx)
+__device__ __forceinline__ uint32_t low_bytes_mask(uint32_t n)   // keep the n (<4) low bytes
 {
-    // idx in [0, 9); small select chain (runs only on header/edge chunks)
-    uint32_t r = h.w[0];
-#pragma unroll
-    for (uint32_t i = 1; i < 9; i++) r = (idx == i) ? h.w[i] : r;
-    return r;
+    return (n >= 4u) ? 0xFFFFFFFFu : ((1u << (8u * n)) - 1u);
 }
 
-__device__ __forceinline__ uint32_t low_bytes_mask(uint32_t n)   // n in [1,3]
+// Payload dword at byte offset r (a multiple of 4) of a datagram payload of L bytes,
+// zero past L.  Reads only the dword that holds byte r, never the next one.
+__device__ __forceinline__ uint32_t pl_dword(const uint8_t *pl, uint32_t r, uint32_t L)
 {
-    return (n >= 4) ? 0xFFFFFFFFu : ((1u << (8 * n)) - 1u);
+    if (r >= L) return 0u;
+    const uint32_t w = ld4(pl + r);
+    return (r + 4u > L) ? (w & low_bytes_mask(L - r)) : w;
 }
 
-// One 16-byte chunk c of datagram k of an event; `pl` = first payload byte of the
-// datagram, L = its payload length.  Returns false when the chunk lies wholly past the
-// datagram end (nothing to store).
-template <bool A4>
-__device__ __forceinline__ bool seg_chunk(u32x4 &v, const HdrWords &h, const uint8_t *pl,
-                                          uint32_t L, uint32_t c)
+// Header dword i (0..8) of the datagram; w5 (bufferOffset) is the only per-datagram word.
+struct SegHdr {
+    uint32_t w0, w1, w2, w3, w4, w6, w7, w8;
+};
+
+__device__ __forceinline__ uint32_t seg_hdr_byte(const SegHdr &h, uint32_t w5, uint32_t q)
 {
-    const uint32_t q0 = 16u * c;
-    const uint32_t dlen = kLBREHdrLen + L;
-    if (q0 >= dlen) return false;
-    if (A4 && c >= 3 && q0 + 16u <= dlen) {
-        v = ld16(pl + (q0 - kLBREHdrLen));
-        return true;
-    }
-    if (A4) {
+    const uint32_t i = q >> 2;
+    uint32_t w = h.w0;
+    w = (i == 1) ? h.w1 : w;
+    w = (i == 2) ? h.w2 : w;
+    w = (i == 3) ? h.w3 : w;
+    w = (i == 4) ? h.w4 : w;
+    w = (i == 5) ? w5 : w;
+    w = (i == 6) ? h.w6 : w;
+    w = (i == 7) ? h.w7 : w;
+    w = (i == 8) ? h.w8 : w;
+    return (w >> (8u * (q & 3u))) & 0xFFu;
+}
+
+// Generic case (event not dword-aligned, or maxPldLen % 4 != 0): byte loads.
+__device__ __forceinline__ u32x4 seg_chunk_bytes(const SegHdr &h, uint32_t w5, const uint8_t *pl,
+                                                 uint32_t L, uint32_t c)
+{
+    uint32_t o[4];
 #pragma unroll
-        for (uint32_t d = 0; d < 4; d++) {
-            const uint32_t q = q0 + 4u * d;
-            uint32_t w;
-            if (q < kLBREHdrLen) {
-                w = hdr_word(h, q >> 2);
-            } else {
-                const uint32_t r = q - kLBREHdrLen;
-                if (r >= L) {
-                    w = 0;
-                } else {
-                    w = ld4(pl + r);
-                    if (r + 4u > L) w &= low_bytes_mask(L - r);
-                }
-            }
-            v[d] = w;
+    for (uint32_t d = 0; d < 4; d++) {
+        uint32_t w = 0;
+#pragma unroll
+        for (uint32_t b = 0; b < 4; b++) {
+            const uint32_t q = 16u * c + 4u * d + b;
+            uint32_t byte = 0;
+            if (q < kLBREHdrLen) byte = seg_hdr_byte(h, w5, q);
+            else if (q - kLBREHdrLen < L) byte = ld1(pl + (q - kLBREHdrLen));
+            w |= byte << (8u * b);
         }
-    } else {
-        // generic byte path: any event alignment, any maxPldLen
-#pragma unroll
-        for (uint32_t d = 0; d < 4; d++) {
-            uint32_t w = 0;
-#pragma unroll
-            for (uint32_t b = 0; b < 4; b++) {
-                const uint32_t q = q0 + 4u * d + b;
-                uint32_t byte;
-                if (q < kLBREHdrLen) byte = (hdr_word(h, q >> 2) >> (8 * (q & 3))) & 0xFFu;
-                else if (q - kLBREHdrLen < L) byte = ld1(pl + (q - kLBREHdrLen));
-                else byte = 0;
-                w |= byte << (8 * b);
-            }
-            v[d] = w;
-        }
+        o[d] = w;
     }
-    return true;
+    u32x4 v;
+    v.x = o[0];
+    v.y = o[1];
+    v.z = o[2];
+    v.w = o[3];
+    return v;
+}
+
+// Drop the s (0..3, lane-varying) lowest dwords of x, shifting the rest down, zero fill.
+__device__ __forceinline__ u32x4 rot_down(u32x4 x, uint32_t s)
+{
+    u32x4 o;
+    o.x = (s == 0u) ? x.x : (s == 1u) ? x.y : (s == 2u) ? x.z : x.w;
+    o.y = (s == 0u) ? x.y : (s == 1u) ? x.z : (s == 2u) ? x.w : 0u;
+    o.z = (s == 0u) ? x.z : (s == 1u) ? x.w : 0u;
+    o.w = (s == 0u) ? x.w : 0u;
+    return o;
+}
+
+// Zero the bytes of o at and past n (n in [0, 16]).
+__device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
+{
+#pragma unroll
+    for (int d = 0; d < 4; d++) {
+        const int vb = (int)n - 4 * d;
+        o[d] = (vb <= 0) ? 0u : (vb < 4) ? (o[d] & low_bytes_mask((uint32_t)vb)) : o[d];
+    }
+    return o;
 }
 
 // grid.x = nEvents * blocksPerEvent; each block owns kBlock*U consecutive 16-byte
 // chunks of ONE event's datagram range (event-major: every event field is a scalar).
+// Datagram k of the event sits at pkts + (pktBase + k) * stride, so chunk j of the
+// event lands at pkts + pktBase*stride + 16*j: the stores of a block are one contiguous
+// run of memory.
+//
+// Chunk c of a datagram with payload pl[0, L): c = 0, 1 are LB / RE header words, c = 2
+// is the RE eventNum low word + payload 0..11, c >= 3 is payload [16c-36, 16c-20).
+// Every lane issues exactly one unconditional 16-byte load per chunk (phase 1) -- the
+// window is slid back so it never leaves the event (a tail chunk reads the 16 bytes
+// that END at its last dword, then shifts them down in registers) -- and only phase 2
+// consumes them.  So no load result sits behind a branch and all U loads of a lane are
+// in flight together.
 template <bool A4, int U>
 __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                      uint32_t blocksPerEvent, int lbVersion,
@@ -121,31 +156,86 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
     const uint32_t j0 = bx * (uint32_t)(kBlock * U);
     if (j0 >= nch) return;
 
-    u32x4 v[U];
-    uint8_t *dst[U];
-    bool st[U];
+    HdrWords hw;
+    lbre_words(hw, lbVersion, ev.entropy, ev.lbTick, ev.dataId, 0u, bytes, ev.eventNum);
+    const SegHdr h{hw.w[0], hw.w[1], hw.w[2], hw.w[3], hw.w[4], hw.w[6], hw.w[7], hw.w[8]};
+    uint8_t *const out = pkts + (uint64_t)ev.pktBase * stride;
+    const uint8_t *const safe = reinterpret_cast<const uint8_t *>(events + e);   // >= 16 valid bytes
+    const float rspc = 1.0f / (float)spc;
+
+    u32x4 x[U];
+    uint32_t jj[U], cc[U], LL[U], kk[U], sh[U];
+    bool rare[U];
+    // ---- phase 1: one load per chunk ----
 #pragma unroll
     for (int u = 0; u < U; u++) {
         const uint32_t j = j0 + (uint32_t)u * kBlock + threadIdx.x;
-        st[u] = false;
-        dst[u] = nullptr;
+        jj[u] = 0xFFFFFFFFu;
+        cc[u] = LL[u] = kk[u] = sh[u] = 0;
+        rare[u] = false;
+        const uint8_t *a = safe;
         if (j < nch) {
-            const uint32_t k = j / spc;
+            // k = j / spc via a float reciprocal and a +-1 correction (exact for j < 2^32)
+            uint32_t k = (uint32_t)((float)j * rspc);
+            if (k * spc > j) k--;
+            else if ((k + 1u) * spc <= j) k++;
             const uint32_t c = j - k * spc;
-            const uint64_t off = (uint64_t)k * maxPld;
-            const uint32_t L = (bytes - off > maxPld) ? maxPld : (uint32_t)(bytes - off);
-            HdrWords h;
-            lbre_words(h, lbVersion, ev.entropy, ev.lbTick, ev.dataId, (uint32_t)off, bytes,
-                       ev.eventNum);
-            const uint64_t p = (uint64_t)ev.pktBase + k;
-            dst[u] = pkts + p * stride + 16u * c;
-            st[u] = seg_chunk<A4>(v[u], h, ev.data + off, L, c);
-            if (c == 0 && lens) lens[p] = kLBREHdrLen + L;
+            const uint32_t off = k * maxPld;
+            const uint32_t L = (bytes - off > maxPld) ? maxPld : bytes - off;
+            if (c == 0u && lens) lens[ev.pktBase + k] = kLBREHdrLen + L;
+            if (16u * c < kLBREHdrLen + L) {          // else: chunk wholly past the datagram end
+                jj[u] = j;
+                cc[u] = c;
+                LL[u] = L;
+                kk[u] = k;
+                const uint8_t *pl = ev.data + off;
+                if (!A4) {
+                    rare[u] = true;
+                } else if (c >= 3u) {
+                    const uint32_t r = 16u * c - kLBREHdrLen;
+                    const uint32_t n = (L - r < 16u) ? L - r : 16u;
+                    const uint32_t rn = (n + 3u) & ~3u;
+                    sh[u] = (16u - rn) >> 2;
+                    a = pl + (r + rn - 16u);
+                } else if (c == 2u) {
+                    if (k > 0u && L >= 12u) a = pl - 4;       // previous datagram's last payload dword
+                    else rare[u] = true;                      // event start / tiny datagram
+                }
+            }
         }
+        x[u] = ld16_nt(a);
     }
+    // ---- phase 2: header words, shifts, tail masks, stores ----
 #pragma unroll
-    for (int u = 0; u < U; u++)
-        if (st[u]) st16(dst[u], v[u]);
+    for (int u = 0; u < U; u++) {
+        if (jj[u] == 0xFFFFFFFFu) continue;
+        const uint32_t c = cc[u], L = LL[u];
+        const uint32_t w5 = bswap32(kk[u] * maxPld);
+        const uint8_t *pl = ev.data + kk[u] * maxPld;
+        u32x4 o;
+        if (rare[u]) {
+            if (!A4) {
+                o = seg_chunk_bytes(h, w5, pl, L, c);
+            } else {        // c == 2 at an event start or in a datagram of < 12 payload bytes
+                o.x = h.w8;
+                o.y = pl_dword(pl, 0u, L);
+                o.z = pl_dword(pl, 4u, L);
+                o.w = pl_dword(pl, 8u, L);
+            }
+        } else if (c >= 3u) {
+            const uint32_t r = 16u * c - kLBREHdrLen;
+            o = rot_down(x[u], sh[u]);
+            if (L - r < 16u) o = keep_low_bytes(o, L - r);
+        } else if (c == 2u) {
+            o = x[u];
+            o.x = h.w8;
+        } else if (c == 1u) {
+            o = u32x4{h.w4, w5, h.w6, h.w7};
+        } else {
+            o = u32x4{h.w0, h.w1, h.w2, h.w3};
+        }
+        st16(out + 16u * jj[u], o);
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -239,12 +329,15 @@ __device__ LookupResult find_or_create(const ReasDev &R, uint64_t ev, uint32_t d
             }
         }
         if (stt == kReady) {
+            // one round trip for the whole key + buffer record (all stored before READY)
             const uint64_t sev = ld_agent(&sl->eventNum);
             const uint32_t sd = ld_agent(&sl->dataId);
+            const uint32_t sb = ld_agent(&sl->bytes);
+            const uint64_t so = ld_agent(&sl->bufOff);
             if (sev == ev && sd == d) {
                 res.slot = h;
-                res.bytes = ld_agent(&sl->bytes);
-                res.bufOff = ld_agent(&sl->bufOff);
+                res.bytes = sb;
+                res.bufOff = so;
                 return res;
             }
         }
@@ -281,14 +374,13 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
 // One lane per datagram.  Consecutive lanes that carry the same (eventNum, dataId) form
 // a run: only the run head touches the event table and only the run tail adds to the
 // event's byte/fragment counter, so the per-event atomics are per run, not per packet.
-__global__ __launch_bounds__(kBlock) void reas_classify(ReasDev R, const uint8_t *__restrict__ pkts,
-                                                        uint32_t stride, const uint32_t *__restrict__ lens,
-                                                        uint32_t n, uint64_t now,
-                                                        PktInfo *__restrict__ info)
+// Executed by one whole wave (all 64 lanes, any subset live); returns the lane's
+// destination record.
+__device__ PktInfo classify_wave(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                 const uint32_t *__restrict__ lens, uint32_t p, bool live, uint64_t now,
+                                 uint32_t shard)
 {
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
     const int lane = threadIdx.x & 63;
-    const bool live = p < n;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
     const uint32_t reo = R.withLB ? kLBHdrLen : 0u;
 
@@ -398,14 +490,11 @@ __global__ __launch_bounds__(kBlock) void reas_classify(ReasDev R, const uint8_t
         }
     }
 
-    if (live) {
-        PktInfo pi;
-        const bool scatter = take && boff != kNoBuf;
-        pi.dst = scatter ? (uint64_t)(R.arena + boff + off) : 0ull;
-        pi.plen = scatter ? pl : 0u;
-        pi.hl = hl;
-        info[p] = pi;
-    }
+    PktInfo pi;
+    const bool scatter = take && boff != kNoBuf;
+    pi.dst = scatter ? (uint64_t)(R.arena + boff + off) : 0ull;
+    pi.plen = scatter ? pl : 0u;
+    pi.hl = hl;
     if (ok && slot == kNoSlot) derr = true;                    // table full / probe timeout
 
     // ---- stats: one atomic per wave per counter ----
@@ -414,74 +503,133 @@ __global__ __launch_bounds__(kBlock) void reas_classify(ReasDev R, const uint8_t
     const uint64_t nder = __builtin_popcountll(__ballot(derr));
     const uint64_t tb = wave_sum_u64(live ? (uint64_t)len : 0ull);
     if (lane == 0) {
-        if (np) atomicAdd(&R.ctl->totalPackets, (unsigned long long)np);
-        if (tb) atomicAdd(&R.ctl->totalBytes, (unsigned long long)tb);
-        if (nbad) atomicAdd(&R.ctl->badHeaderDiscards, (unsigned long long)nbad);
-        if (nder) atomicAdd(&R.ctl->dataErrCnt, (unsigned long long)nder);
+        ReasShard *sh = R.shards + (shard % kShards);
+        if (np) atomicAdd(&sh->totalPackets, (unsigned long long)np);
+        if (tb) atomicAdd(&sh->totalBytes, (unsigned long long)tb);
+        if (nbad) atomicAdd(&sh->badHeaderDiscards, (unsigned long long)nbad);
+        if (nder) atomicAdd(&sh->dataErrCnt, (unsigned long long)nder);
     }
+    return pi;
 }
 
 // ---------------------------------------------------------------------------------
 // reassembly: payload scatter
 
-__device__ __forceinline__ void copy_edge(uint8_t *lo, uint8_t *hi, const uint8_t *src)
+__device__ __noinline__ void copy_bytes(uint8_t *lo, uint8_t *hi, const uint8_t *src)
 {
-    // [lo, hi) inside one 16-byte destination chunk; src corresponds to lo.
-    const bool congruent = (((uintptr_t)lo ^ (uintptr_t)src) & 3u) == 0;
-    while (lo < hi) {
-        if (congruent && (((uintptr_t)lo & 3u) == 0) && lo + 4 <= hi) {
-            st4(lo, ld4(src));
-            lo += 4;
-            src += 4;
-        } else {
-            st1(lo++, ld1(src++));
-        }
-    }
+    // rare path: destination/source not dword-congruent, or a one-chunk datagram
+    while (lo < hi) st1(lo++, ld1(src++));
 }
 
-// Flat over the packet arena's 16-byte chunks: chunk c of packet p writes destination
-// chunk (dst0 & ~15) + 16c, i.e. destination-aligned 16-byte stores.
+// reas_kernel: one block = G consecutive datagrams (G <= 64, chosen so a block moves
+// ~64-128 KiB).  Wave 0 classifies them (one lane per datagram, classify_wave) and
+// leaves each datagram's destination record in LDS; then all 256 threads copy the G
+// payloads, flat over the block's G*spc 16-byte chunks.  Chunk c of datagram p writes
+// destination chunk cb = (d0 & ~15) + 16c (destination-aligned stores).  Per chunk one
+// unconditional 16-byte load (phase 1) of the source window that maps onto cb; a head
+// chunk's window starts in the datagram's own header bytes, a tail chunk's window is slid
+// back to end at its last dword (then shifted down in registers), so no read leaves the
+// datagram.  Phase 2 stores whole chunks, or whole dwords at the edges; only the event's
+// last partial dword is written bytewise.  Non-dword-congruent datagrams (offsets from
+// the wire that are not multiples of 4) and one-chunk payloads take a byte loop.
 template <int U>
-__global__ __launch_bounds__(kBlock) void reas_scatter(const PktInfo *__restrict__ info,
-                                                       const uint8_t *__restrict__ pkts,
-                                                       uint32_t stride, uint32_t spc,
-                                                       uint32_t nChunks)
+__global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+                                                      uint32_t stride, const uint32_t *__restrict__ lens,
+                                                      uint32_t n, uint64_t now, uint32_t G)
 {
-    const uint32_t base = blockIdx.x * (uint32_t)(kBlock * U) + threadIdx.x;
-    u32x4 v[U];
-    uint8_t *dst[U];
-    bool st[U];
+    __shared__ PktInfo sinfo[64];
+    const uint32_t g0 = blockIdx.x * G;
+    const uint32_t gn = (n - g0 < G) ? n - g0 : G;
+    if (threadIdx.x < 64) {
+        const uint32_t lane = threadIdx.x;
+        const PktInfo pi = classify_wave(R, pkts, stride, lens, g0 + lane, lane < gn, now, blockIdx.x);
+        sinfo[lane] = pi;
+    }
+    __syncthreads();
+
+    const uint32_t spc = stride >> 4;
+    const uint32_t nch = gn * spc;
+    const float rspc = 1.0f / (float)spc;
+    const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
+    const uint8_t *const safe = bpk;
+    enum : uint32_t { kNone = 0, kFull = 1, kHead = 2, kTail = 3, kSlow = 4 };
+
+    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+        u32x4 x[U];
+        uint32_t kind[U], sh[U], pp[U], cc[U];
 #pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t i = base + (uint32_t)u * kBlock;
-        st[u] = false;
-        dst[u] = nullptr;
-        if (i < nChunks) {
-            const uint32_t p = i / spc;
-            const uint32_t c = i - p * spc;
-            const PktInfo pi = info[p];
-            if (pi.plen) {
-                uint8_t *d0 = reinterpret_cast<uint8_t *>(pi.dst);
-                uint8_t *d1 = d0 + pi.plen;
-                uint8_t *cb = reinterpret_cast<uint8_t *>(((uintptr_t)d0 & ~(uintptr_t)15) + 16u * c);
-                if (cb < d1) {
-                    const uint8_t *s0 = pkts + (uint64_t)p * stride + pi.hl;
-                    if (cb >= d0 && cb + 16 <= d1 && ((((uintptr_t)d0) ^ ((uintptr_t)s0)) & 3u) == 0) {
-                        v[u] = ld16(s0 + (cb - d0));
-                        dst[u] = cb;
-                        st[u] = true;
-                    } else {
-                        uint8_t *lo = cb < d0 ? d0 : cb;
-                        uint8_t *hi = (cb + 16 < d1) ? cb + 16 : d1;
-                        copy_edge(lo, hi, s0 + (lo - d0));
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            kind[u] = kNone;
+            sh[u] = 0;
+            pp[u] = 0;
+            cc[u] = 0;
+            const uint8_t *a = safe;
+            if (i < nch) {
+                uint32_t p = (uint32_t)((float)i * rspc);
+                if (p * spc > i) p--;
+                else if ((p + 1u) * spc <= i) p++;
+                const uint32_t c = i - p * spc;
+                pp[u] = p;
+                cc[u] = c;
+                const PktInfo pi = sinfo[p];
+                if (pi.plen) {
+                    const uintptr_t d0 = (uintptr_t)pi.dst, d1 = d0 + pi.plen;
+                    const uintptr_t cb = (d0 & ~(uintptr_t)15) + 16u * c;
+                    if (cb < d1) {
+                        const uint8_t *s0 = bpk + (uint64_t)p * stride + pi.hl;
+                        const bool congruent = ((d0 ^ (uintptr_t)s0) & 3u) == 0;
+                        const bool head = cb < d0, tail = cb + 16 > d1;
+                        if (!congruent || (head && tail)) {
+                            kind[u] = kSlow;
+                        } else if (tail) {
+                            const uint32_t rn = ((uint32_t)(d1 - cb) + 3u) & ~3u;
+                            sh[u] = (16u - rn) >> 2;
+                            a = s0 + (cb - d0) + rn - 16;
+                            kind[u] = kTail;
+                        } else {
+                            a = s0 + (intptr_t)(cb - d0);
+                            kind[u] = head ? kHead : kFull;
+                        }
                     }
                 }
             }
+            x[u] = ld16(a);
+        }
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            if (kind[u] == kNone) continue;
+            const PktInfo pi = sinfo[pp[u]];
+            uint8_t *const d0 = reinterpret_cast<uint8_t *>(pi.dst);
+            uint8_t *const d1 = d0 + pi.plen;
+            uint8_t *const cb = reinterpret_cast<uint8_t *>(((uintptr_t)d0 & ~(uintptr_t)15) + 16u * cc[u]);
+            if (kind[u] == kFull) {
+                st16_nt(cb, x[u]);
+            } else if (kind[u] == kHead) {
+                const uint32_t lo = (uint32_t)(d0 - cb) >> 2;
+#pragma unroll
+                for (uint32_t d = 1; d < 4; d++)
+                    if (d >= lo) st4(cb + 4 * d, x[u][d]);
+            } else if (kind[u] == kTail) {
+                const u32x4 o = rot_down(x[u], sh[u]);
+                const uint32_t nb = (uint32_t)(d1 - cb);
+#pragma unroll
+                for (uint32_t d = 0; d < 4; d++) {
+                    const int vb = (int)nb - 4 * (int)d;
+                    if (vb >= 4) {
+                        st4(cb + 4 * d, o[d]);
+                    } else if (vb > 0) {
+                        for (int b = 0; b < vb; b++) st1(cb + 4 * d + b, (uint8_t)(o[d] >> (8 * b)));
+                    }
+                }
+            } else {
+                const uint8_t *s0 = bpk + (uint64_t)pp[u] * stride + pi.hl;
+                uint8_t *lo = cb < d0 ? d0 : cb;
+                uint8_t *hi = (cb + 16 < d1) ? cb + 16 : d1;
+                copy_bytes(lo, hi, s0 + (lo - d0));
+            }
         }
     }
-#pragma unroll
-    for (int u = 0; u < U; u++)
-        if (st[u]) st16(dst[u], v[u]);
 }
 
 // ---------------------------------------------------------------------------------
@@ -538,6 +686,7 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     constexpr int U = 4;
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
+    if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32
     const uint32_t bpe = cdiv(chunks, (uint64_t)kBlock * U);
     const uint64_t grid = (uint64_t)bpe * nEvents;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -551,18 +700,16 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
 }
 
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, PktInfo *info,
-                             hipStream_t stream)
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
 {
     constexpr int U = 4;
     if (n == 0) return hipSuccess;
-    hipLaunchKernelGGL(reas_classify, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts,
-                       stride, lens, n, now, info);
+    // datagrams per block: about 6K 16-byte chunks (96 KiB of payload) per block, <= 64
     const uint32_t spc = stride >> 4;
-    const uint64_t chunks = (uint64_t)n * spc;
-    if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((reas_scatter<U>), dim3(cdiv(chunks, (uint64_t)kBlock * U)), dim3(kBlock), 0,
-                       stream, info, pkts, stride, spc, (uint32_t)chunks);
+    uint32_t G = 64;
+    while (G > 1 && G * spc > 6144u) G >>= 1;
+    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
+                       now, G);
     return hipGetLastError();
 }
 

@@ -26,13 +26,10 @@ static_assert(sizeof(ReasSlot) == 64, "slot is one 64-byte line");
 constexpr uint32_t kAccFragShift = 36;
 constexpr uint64_t kAccBytesMask = (1ull << kAccFragShift) - 1ull;
 
-// Counters (Reassembler::AtomicStats, e2sarDPReassembler.hpp:102-122) + allocator state.
+// Per-event counters (Reassembler::AtomicStats, e2sarDPReassembler.hpp:102-122) + allocator
+// state; the per-packet counters live in ReasShard.
 struct ReasCtl {
     unsigned long long arenaTop;
-    unsigned long long totalPackets;
-    unsigned long long totalBytes;
-    unsigned long long badHeaderDiscards;
-    unsigned long long dataErrCnt;
     unsigned long long eventSuccess;
     unsigned long long enqueueLoss;
     unsigned long long reassemblyLoss;
@@ -44,10 +41,23 @@ struct ReasCtl {
     uint64_t pad[4];
 };
 
+// Per-packet counters are sharded (one 128-byte line per shard, shard = block % kShards)
+// so thousands of waves do not serialise on one address; the host sums the shards.
+constexpr uint32_t kShards = 64;
+struct ReasShard {
+    unsigned long long totalPackets;
+    unsigned long long totalBytes;
+    unsigned long long badHeaderDiscards;
+    unsigned long long dataErrCnt;
+    unsigned long long pad[12];
+};
+static_assert(sizeof(ReasShard) == 128, "one shard per 128-byte line");
+
 // Everything a reassembly kernel needs, passed by value.
 struct ReasDev {
     ReasSlot *slots;
     ReasCtl *ctl;
+    ReasShard *shards;
     e2sar_hip_event_rec *completed;
     e2sar_hip_lost_rec *lost;
     uint8_t *arena;
@@ -58,7 +68,7 @@ struct ReasDev {
     int withLB;
 };
 
-// Per-datagram result of classification, consumed by the scatter kernel.
+// Per-datagram result of classification (held in LDS between the two phases of reas_kernel).
 struct PktInfo {
     uint64_t dst;     // device address of the payload's destination (0 = drop)
     uint32_t plen;    // payload bytes
@@ -71,8 +81,7 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream);
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, PktInfo *info,
-                             hipStream_t stream);
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
 hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);
 hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stream);
 

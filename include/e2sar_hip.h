@@ -49,10 +49,15 @@ int e2sar_hip_abi_version(void);
 const char *e2sar_hip_last_error(void);
 
 typedef struct e2sar_hip_ctx e2sar_hip_ctx;
-/* Bind a device.  `stream` is a hipStream_t (NULL = the context creates its own
- * non-blocking stream).  Replaces the per-Segmenter/Reassembler thread state
- * (e2sarDPSegmenter.hpp:213-260, e2sarDPReassembler.hpp:206-240). */
+/* Bind a device and a stream.  `stream` is the hipStream_t every call of this context
+ * runs on when the call's own `stream` argument is NULL; NULL here means the device's
+ * default stream.  Replaces the per-Segmenter/Reassembler thread state
+ * (e2sarDPSegmenter.hpp:213-260, e2sarDPReassembler.hpp:206-240): one context per
+ * sending/receiving thread gives the same concurrency without shared mutable state. */
 int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out);
+/* A non-blocking stream for callers without a HIP toolchain. */
+int e2sar_hip_stream_create(int device, void **out);
+int e2sar_hip_stream_destroy(void *stream);
 void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx);
 void *e2sar_hip_ctx_stream(e2sar_hip_ctx *ctx);
 int e2sar_hip_ctx_device(e2sar_hip_ctx *ctx);

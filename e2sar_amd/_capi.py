@@ -10,7 +10,7 @@ import ctypes as C
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libe2sar_hip.so")
+LIB_PATH = os.environ.get("E2SAR_HIP_LIB") or os.path.join(_HERE, "lib", "libe2sar_hip.so")
 
 # status codes = -(E2SARErrorc) (reference include/e2sarError.hpp:23-39)
 OK = 0

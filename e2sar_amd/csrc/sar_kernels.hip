@@ -23,6 +23,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
+#ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
+#define E2SAR_REAS_CHUNKS_PER_BLOCK 4096u
+#endif
 
 // Global-address-space accessors: the event/packet/arena pointers reach the kernels
 // through descriptor tables, so without these hipcc falls back to flat_* accesses.
@@ -40,6 +43,11 @@ __device__ __forceinline__ u32x4 ld16_nt(const uint8_t *p)
     return __builtin_nontemporal_load((const E2SAR_GLOBAL u32x4_a4 *)(p));
 }
 __device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4 *)(p)); }
+// 16-byte non-temporal store at a dword-aligned (not 16-byte-aligned) address
+__device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v)
+{
+    __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4_a4 *)(p));
+}
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
 
 // ---------------------------------------------------------------------------------
@@ -371,42 +379,64 @@ __device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
     return v;   // valid in lane 0
 }
 
-// One lane per datagram.  Consecutive lanes that carry the same (eventNum, dataId) form
-// a run: only the run head touches the event table and only the run tail adds to the
-// event's byte/fragment counter, so the per-event atomics are per run, not per packet.
-// Executed by one whole wave (all 64 lanes, any subset live); returns the lane's
-// destination record.
-__device__ PktInfo classify_wave(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
-                                 const uint32_t *__restrict__ lens, uint32_t p, bool live, uint64_t now,
-                                 uint32_t shard)
+// Raw header words of one datagram, loaded before the payload loads of the block so the
+// classification chain overlaps them.
+struct RawHdr {
+    uint32_t len;
+    u32x4 re;        // RE header dwords 0..3
+    uint32_t re4;    // RE header dword 4 (eventNum low word)
+};
+
+__device__ __forceinline__ RawHdr load_hdr(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                           const uint32_t *__restrict__ lens, uint32_t p)
+{
+    const uint8_t *re = pkts + (uint64_t)p * stride + (R.withLB ? kLBHdrLen : 0u);   // 16-byte aligned
+    RawHdr h;
+    h.len = lens[p];
+    h.re = ld16(re);
+    h.re4 = ld4(re + 16);
+    return h;
+}
+
+// Per-lane classification result; the run tail's counter update is issued during
+// classification and its return value consumed only after the payload stores.
+struct Classified {
+    PktInfo info;
+    uint64_t ev;
+    uint64_t boff;
+    unsigned long long old;   // value returned by the run tail's atomic add
+    uint32_t d, slot, sbytes, rb, rc;
+    bool tailAdd;
+};
+
+// Executed by one whole wave (all 64 lanes, any subset live).  Consecutive lanes that
+// carry the same (eventNum, dataId) form a run: only the run head touches the event
+// table and only the run tail adds to the event's byte/fragment counter, so the
+// per-event atomics are per run, not per datagram.
+__device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
+                                    uint64_t now, uint32_t shard)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
-    const uint32_t reo = R.withLB ? kLBHdrLen : 0u;
 
-    uint32_t len = 0;
+    const uint32_t len = live ? raw.len : 0u;
     bool ok = false, bad = false, derr = false;
     uint64_t ev = 0;
     uint32_t d = 0, off = 0, blen = 0, pl = 0;
     if (live) {
-        len = lens[p];
         if (len < hl) {
             bad = true;                                       // too short to hold the headers
         } else if (len > stride) {
             derr = true;                                      // datagram overruns its slot
+        } else if (!re_valid(raw.re.x)) {
+            bad = true;                                       // cpp:351-357
         } else {
-            const uint32_t *re = reinterpret_cast<const uint32_t *>(pkts + (uint64_t)p * stride + reo);
-            const uint32_t w0 = re[0], w1 = re[1], w2 = re[2], w3 = re[3], w4 = re[4];
-            if (!re_valid(w0)) {
-                bad = true;                                   // cpp:351-357
-            } else {
-                d = bswap16(w0 >> 16);
-                off = bswap32(w1);
-                blen = bswap32(w2);
-                ev = ((uint64_t)bswap32(w3) << 32) | bswap32(w4);
-                pl = len - hl;
-                ok = true;
-            }
+            d = bswap16(raw.re.x >> 16);
+            off = bswap32(raw.re.y);
+            blen = bswap32(raw.re.z);
+            ev = ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4);
+            pl = len - hl;
+            ok = true;
         }
     }
 
@@ -435,7 +465,7 @@ __device__ PktInfo classify_wave(const ReasDev &R, const uint8_t *__restrict__ p
         derr = true;
     }
     // segmented sums over the run (inclusive scans, then difference at the head)
-    uint32_t xb = take ? pl : 0u, xc = take ? 1u : 0u;
+    const uint32_t xb = take ? pl : 0u, xc = take ? 1u : 0u;
     uint32_t ib = xb, ic = xc;
 #pragma unroll
     for (unsigned s = 1; s < 64; s <<= 1) {
@@ -446,58 +476,29 @@ __device__ PktInfo classify_wave(const ReasDev &R, const uint8_t *__restrict__ p
         }
     }
     const uint32_t hb = __shfl(ib - xb, myhead), hc = __shfl(ic - xc, myhead);
-    if (tail && slot != kNoSlot) {
-        const uint32_t rb = ib - hb, rc = ic - hc;
-        ReasSlot *sl = R.slots + slot;
-        const uint64_t add = ((uint64_t)rc << kAccFragShift) | rb;
-        const uint64_t old = atomicAdd(&sl->acc, (unsigned long long)add);
-        const uint64_t nb = (old & kAccBytesMask) + rb;
-        if (rc > 0 && nb == sbytes) {                          // curBytes == bytes (cpp:403)
-            st_agent(&sl->state, (uint32_t)kDone);             // erase from the map (cpp:409)
-            atomicAdd(&R.ctl->eventSuccess, 1ull);             // cpp:426
-            atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
-            const uint32_t frags = (uint32_t)(old >> kAccFragShift) + rc;
-            bool lostOnEnqueue = (boff == kNoBuf);
-            if (!lostOnEnqueue) {
-                const uint32_t idx = atomicAdd(&R.ctl->nCompleted, 1u);
-                if (idx < R.queueCapacity) {
-                    e2sar_hip_event_rec rec;
-                    rec.eventNum = ev;
-                    rec.arenaOffset = boff;
-                    rec.bytes = sbytes;
-                    rec.dataId = (uint16_t)d;
-                    rec.flags = 0;
-                    rec.numFragments = frags;
-                    rec.reserved = 0;
-                    R.completed[idx] = rec;
-                } else {
-                    lostOnEnqueue = true;                      // queue full (hpp:140-145)
-                }
-            }
-            if (lostOnEnqueue) {
-                atomicAdd(&R.ctl->enqueueLoss, 1ull);
-                const uint32_t li = atomicAdd(&R.ctl->nLost, 1u);
-                if (li < R.lostCapacity) {
-                    e2sar_hip_lost_rec lr2;
-                    lr2.eventNum = ev;
-                    lr2.numFragments = frags;
-                    lr2.dataId = (uint16_t)d;
-                    lr2.enqueueLoss = 1;
-                    lr2.reserved = 0;
-                    R.lost[li] = lr2;
-                }
-            }
-        }
+
+    Classified out;
+    out.ev = ev;
+    out.d = d;
+    out.slot = slot;
+    out.sbytes = sbytes;
+    out.boff = boff;
+    out.rb = ib - hb;
+    out.rc = ic - hc;
+    out.old = 0;
+    out.tailAdd = tail && slot != kNoSlot;
+    if (out.tailAdd) {
+        const uint64_t add = ((uint64_t)out.rc << kAccFragShift) | out.rb;
+        out.old = atomicAdd(&R.slots[slot].acc, (unsigned long long)add);   // consumed in classify_finish
     }
 
-    PktInfo pi;
     const bool scatter = take && boff != kNoBuf;
-    pi.dst = scatter ? (uint64_t)(R.arena + boff + off) : 0ull;
-    pi.plen = scatter ? pl : 0u;
-    pi.hl = hl;
+    out.info.dst = scatter ? (uint64_t)(R.arena + boff + off) : 0ull;
+    out.info.plen = scatter ? pl : 0u;
+    out.info.hl = hl;
     if (ok && slot == kNoSlot) derr = true;                    // table full / probe timeout
 
-    // ---- stats: one atomic per wave per counter ----
+    // ---- stats: one atomic per wave per counter, sharded ----
     const uint64_t np = __builtin_popcountll(__ballot(live));
     const uint64_t nbad = __builtin_popcountll(__ballot(bad));
     const uint64_t nder = __builtin_popcountll(__ballot(derr));
@@ -509,29 +510,72 @@ __device__ PktInfo classify_wave(const ReasDev &R, const uint8_t *__restrict__ p
         if (nbad) atomicAdd(&sh->badHeaderDiscards, (unsigned long long)nbad);
         if (nder) atomicAdd(&sh->dataErrCnt, (unsigned long long)nder);
     }
-    return pi;
+    return out;
+}
+
+// Completion (cpp:403-427): the run tail whose add brought curBytes to the event length.
+__device__ __forceinline__ void classify_finish(const ReasDev &R, const Classified &c)
+{
+    if (!c.tailAdd) return;
+    const uint64_t nb = (c.old & kAccBytesMask) + c.rb;
+    if (!(c.rc > 0 && nb == c.sbytes)) return;                // curBytes == bytes (cpp:403)
+    ReasSlot *sl = R.slots + c.slot;
+    st_agent(&sl->state, (uint32_t)kDone);                     // erase from the map (cpp:409)
+    atomicAdd(&R.ctl->eventSuccess, 1ull);                     // cpp:426
+    atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
+    const uint32_t frags = (uint32_t)(c.old >> kAccFragShift) + c.rc;
+    bool lostOnEnqueue = (c.boff == kNoBuf);
+    if (!lostOnEnqueue) {
+        const uint32_t idx = atomicAdd(&R.ctl->nCompleted, 1u);
+        if (idx < R.queueCapacity) {
+            e2sar_hip_event_rec rec;
+            rec.eventNum = c.ev;
+            rec.arenaOffset = c.boff;
+            rec.bytes = c.sbytes;
+            rec.dataId = (uint16_t)c.d;
+            rec.flags = 0;
+            rec.numFragments = frags;
+            rec.reserved = 0;
+            R.completed[idx] = rec;
+        } else {
+            lostOnEnqueue = true;                              // queue full (hpp:140-145)
+        }
+    }
+    if (lostOnEnqueue) {
+        atomicAdd(&R.ctl->enqueueLoss, 1ull);
+        const uint32_t li = atomicAdd(&R.ctl->nLost, 1u);
+        if (li < R.lostCapacity) {
+            e2sar_hip_lost_rec lr;
+            lr.eventNum = c.ev;
+            lr.numFragments = frags;
+            lr.dataId = (uint16_t)c.d;
+            lr.enqueueLoss = 1;
+            lr.reserved = 0;
+            R.lost[li] = lr;
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------------
-// reassembly: payload scatter
+// reassembly: one fused kernel
 
-__device__ __noinline__ void copy_bytes(uint8_t *lo, uint8_t *hi, const uint8_t *src)
+__device__ __noinline__ void store_bytes(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
 {
-    // rare path: destination/source not dword-congruent, or a one-chunk datagram
-    while (lo < hi) st1(lo++, ld1(src++));
+    // bytes [lo, hi) of the 16-byte register chunk v to dst + (lo..hi); rare path
+    for (uint32_t b = lo; b < hi; b++) st1(dst + b, (uint8_t)(v[b >> 2] >> (8u * (b & 3u))));
 }
 
-// reas_kernel: one block = G consecutive datagrams (G <= 64, chosen so a block moves
-// ~64-128 KiB).  Wave 0 classifies them (one lane per datagram, classify_wave) and
-// leaves each datagram's destination record in LDS; then all 256 threads copy the G
-// payloads, flat over the block's G*spc 16-byte chunks.  Chunk c of datagram p writes
-// destination chunk cb = (d0 & ~15) + 16c (destination-aligned stores).  Per chunk one
-// unconditional 16-byte load (phase 1) of the source window that maps onto cb; a head
-// chunk's window starts in the datagram's own header bytes, a tail chunk's window is slid
-// back to end at its last dword (then shifted down in registers), so no read leaves the
-// datagram.  Phase 2 stores whole chunks, or whole dwords at the edges; only the event's
-// last partial dword is written bytewise.  Non-dword-congruent datagrams (offsets from
-// the wire that are not multiples of 4) and one-chunk payloads take a byte loop.
+// reas_kernel: one block = G consecutive datagrams, G*spc <= 256*U 16-byte chunks, so
+// each thread owns at most U chunks of SOURCE-aligned datagram bytes.
+//   1. wave 0 issues the header loads of the G datagrams;
+//   2. every thread issues its U 16-byte payload loads (aligned, inside the datagram
+//      slots -- no classification needed to know where to read);
+//   3. wave 0 classifies (event table lookup/insert, run sums, counter atomics) while
+//      those loads are in flight, and leaves each datagram's destination in LDS;
+//   4. every thread stores its chunks to event + bufferOffset + (16c - header): whole
+//      16-byte stores inside the payload, whole dwords at the two edges, bytes only for
+//      a sub-dword event tail or a datagram whose offset is not dword-congruent;
+//   5. the run tails complete events (their atomic results are consumed last).
 template <int U>
 __global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                       uint32_t stride, const uint32_t *__restrict__ lens,
@@ -540,96 +584,71 @@ __global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *
     __shared__ PktInfo sinfo[64];
     const uint32_t g0 = blockIdx.x * G;
     const uint32_t gn = (n - g0 < G) ? n - g0 : G;
-    if (threadIdx.x < 64) {
-        const uint32_t lane = threadIdx.x;
-        const PktInfo pi = classify_wave(R, pkts, stride, lens, g0 + lane, lane < gn, now, blockIdx.x);
-        sinfo[lane] = pi;
-    }
-    __syncthreads();
+    const bool w0 = threadIdx.x < 64;
+    const uint32_t lane = threadIdx.x & 63u;
+
+    // every wave issues the (cached) header loads so no load result crosses a branch
+    const RawHdr raw = load_hdr(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
 
     const uint32_t spc = stride >> 4;
     const uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
-    const uint8_t *const safe = bpk;
-    enum : uint32_t { kNone = 0, kFull = 1, kHead = 2, kTail = 3, kSlow = 4 };
-
-    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
-        u32x4 x[U];
-        uint32_t kind[U], sh[U], pp[U], cc[U];
+    u32x4 x[U];
+    uint32_t pp[U], cc[U];
+    auto issue = [&](uint32_t r0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
-            kind[u] = kNone;
-            sh[u] = 0;
-            pp[u] = 0;
-            cc[u] = 0;
-            const uint8_t *a = safe;
-            if (i < nch) {
-                uint32_t p = (uint32_t)((float)i * rspc);
-                if (p * spc > i) p--;
-                else if ((p + 1u) * spc <= i) p++;
-                const uint32_t c = i - p * spc;
-                pp[u] = p;
-                cc[u] = c;
-                const PktInfo pi = sinfo[p];
-                if (pi.plen) {
-                    const uintptr_t d0 = (uintptr_t)pi.dst, d1 = d0 + pi.plen;
-                    const uintptr_t cb = (d0 & ~(uintptr_t)15) + 16u * c;
-                    if (cb < d1) {
-                        const uint8_t *s0 = bpk + (uint64_t)p * stride + pi.hl;
-                        const bool congruent = ((d0 ^ (uintptr_t)s0) & 3u) == 0;
-                        const bool head = cb < d0, tail = cb + 16 > d1;
-                        if (!congruent || (head && tail)) {
-                            kind[u] = kSlow;
-                        } else if (tail) {
-                            const uint32_t rn = ((uint32_t)(d1 - cb) + 3u) & ~3u;
-                            sh[u] = (16u - rn) >> 2;
-                            a = s0 + (cb - d0) + rn - 16;
-                            kind[u] = kTail;
-                        } else {
-                            a = s0 + (intptr_t)(cb - d0);
-                            kind[u] = head ? kHead : kFull;
-                        }
-                    }
-                }
-            }
-            x[u] = ld16(a);
+            const uint32_t ic = (i < nch) ? i : 0u;
+            uint32_t p = (uint32_t)((float)ic * rspc);
+            if (p * spc > ic) p--;
+            else if ((p + 1u) * spc <= ic) p++;
+            pp[u] = p;
+            cc[u] = ic - p * spc;
+            x[u] = ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
         }
+    };
+    issue(0);                          // round 0 is in flight while wave 0 classifies
+
+    Classified cl{};
+    if (w0) {
+        cl = classify_wave(R, raw, stride, lane < gn, now, blockIdx.x);
+        sinfo[lane] = cl.info;
+    }
+    __syncthreads();
+
+    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+        if (r0) issue(r0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            if (kind[u] == kNone) continue;
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            if (i >= nch) continue;
             const PktInfo pi = sinfo[pp[u]];
-            uint8_t *const d0 = reinterpret_cast<uint8_t *>(pi.dst);
-            uint8_t *const d1 = d0 + pi.plen;
-            uint8_t *const cb = reinterpret_cast<uint8_t *>(((uintptr_t)d0 & ~(uintptr_t)15) + 16u * cc[u]);
-            if (kind[u] == kFull) {
-                st16_nt(cb, x[u]);
-            } else if (kind[u] == kHead) {
-                const uint32_t lo = (uint32_t)(d0 - cb) >> 2;
+            if (pi.plen == 0) continue;
+            // datagram bytes [16c, 16c+16) against the payload [hl, hl+plen)
+            const uint32_t q0 = 16u * cc[u];
+            const uint32_t pend = pi.hl + pi.plen;
+            if (q0 >= pend || q0 + 16u <= pi.hl) continue;
+            const uint32_t lo = (q0 < pi.hl) ? pi.hl - q0 : 0u;             // first chunk byte to keep
+            const uint32_t hi = (q0 + 16u <= pend) ? 16u : pend - q0;        // one past the last
+            uint8_t *dst = reinterpret_cast<uint8_t *>(pi.dst) + q0 - pi.hl;  // where chunk byte 0 goes
+            const bool congruent = ((pi.dst - pi.hl) & 3u) == 0;
+            if (lo == 0 && hi == 16u && congruent) {
+                st16u_nt(dst, x[u]);
+            } else if (congruent) {
 #pragma unroll
-                for (uint32_t d = 1; d < 4; d++)
-                    if (d >= lo) st4(cb + 4 * d, x[u][d]);
-            } else if (kind[u] == kTail) {
-                const u32x4 o = rot_down(x[u], sh[u]);
-                const uint32_t nb = (uint32_t)(d1 - cb);
-#pragma unroll
-                for (uint32_t d = 0; d < 4; d++) {
-                    const int vb = (int)nb - 4 * (int)d;
-                    if (vb >= 4) {
-                        st4(cb + 4 * d, o[d]);
-                    } else if (vb > 0) {
-                        for (int b = 0; b < vb; b++) st1(cb + 4 * d + b, (uint8_t)(o[d] >> (8 * b)));
-                    }
-                }
+                for (uint32_t d = 0; d < 4; d++)
+                    if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, x[u][d]);
+                const uint32_t t = hi & ~3u;                               // sub-dword event tail
+                if (t < hi && t >= lo) store_bytes(dst, x[u], t, hi);
             } else {
-                const uint8_t *s0 = bpk + (uint64_t)pp[u] * stride + pi.hl;
-                uint8_t *lo = cb < d0 ? d0 : cb;
-                uint8_t *hi = (cb + 16 < d1) ? cb + 16 : d1;
-                copy_bytes(lo, hi, s0 + (lo - d0));
+                store_bytes(dst, x[u], lo, hi);
             }
         }
     }
+
+    if (w0) classify_finish(R, cl);
 }
 
 // ---------------------------------------------------------------------------------
@@ -704,10 +723,11 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
 {
     constexpr int U = 4;
     if (n == 0) return hipSuccess;
-    // datagrams per block: about 6K 16-byte chunks (96 KiB of payload) per block, <= 64
+    // datagrams per block: at most E2SAR_REAS_CHUNKS_PER_BLOCK 16-byte chunks (64 KiB), <= 64
+    // (tools/ab_chunks.sh: 2K-chunk blocks lose ~8 %, 1K-chunk blocks ~30 %, 4K-12K equal)
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > 6144u) G >>= 1;
+    while (G > 1 && G * spc > E2SAR_REAS_CHUNKS_PER_BLOCK) G >>= 1;
     hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
                        now, G);
     return hipGetLastError();

@@ -22,3 +22,25 @@ clean:
 	$(MAKE) -C oracle clean
 
 .PHONY: all oracle clean
+
+# ---- reference-shaped C++ facade (pure C++ over the C ABI) ----
+CXX ?= g++
+CXXFLAGS ?= -O2 -std=c++17 -fPIC -Wall -Wextra -Wno-unused-parameter
+HOST_SRCS := e2sar_amd/csrc/host/util.cpp e2sar_amd/csrc/host/segmenter.cpp e2sar_amd/csrc/host/reassembler.cpp
+HOST_HDRS := include/e2sar_amd/e2sar.hpp e2sar_amd/csrc/host/host_common.hpp include/e2sar_hip.h
+
+$(LIBDIR)/libe2sar_amd.so: $(HOST_SRCS) $(HOST_HDRS) $(LIBDIR)/libe2sar_hip.so
+	$(CXX) $(CXXFLAGS) -Iinclude -Ie2sar_amd/csrc/host -shared -o $@ $(HOST_SRCS) \
+		-L$(LIBDIR) -le2sar_hip -Wl,-rpath,'$$ORIGIN' -lpthread
+
+all: $(LIBDIR)/libe2sar_amd.so
+
+# ---- e2sar_py: the reference's Python module surface, over the C++ facade ----
+PYEXT := $(shell python3 -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+PYINC := $(shell python3 -c "import sysconfig,pybind11;print('-I'+sysconfig.get_paths()['include'],'-I'+pybind11.get_include())")
+
+e2sar_amd/e2sar_py$(PYEXT): e2sar_amd/csrc/host/py_e2sar.cpp $(HOST_HDRS) include/e2sar_amd/e2sarHeaders.hpp $(LIBDIR)/libe2sar_amd.so
+	$(CXX) $(CXXFLAGS) -fvisibility=hidden $(PYINC) -Iinclude -shared -o $@ e2sar_amd/csrc/host/py_e2sar.cpp \
+		-L$(LIBDIR) -le2sar_amd -le2sar_hip -Wl,-rpath,'$$ORIGIN/lib'
+
+all: e2sar_amd/e2sar_py$(PYEXT)

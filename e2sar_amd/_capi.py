@@ -47,7 +47,12 @@ class ReasConfig(C.Structure):
         ("queueCapacity", C.c_uint32),
         ("lostCapacity", C.c_uint32),
         ("arenaBytes", C.c_uint64),
+        ("flags", C.c_uint32),
+        ("reserved", C.c_uint32),
     ]
+
+
+REAS_COMPACTABLE = 1
 
 
 class EventRec(C.Structure):
@@ -120,6 +125,8 @@ SIGNATURES = {
     "e2sar_hip_memcpy_h2d": (i, [vp, vp, vp, sz]),
     "e2sar_hip_memcpy_d2h": (i, [vp, vp, vp, sz]),
     "e2sar_hip_memset_d": (i, [vp, vp, i, sz]),
+    "e2sar_hip_memcpy_async": (i, [vp, vp, vp, sz, i, vp]),
+    "e2sar_hip_stream_sync": (i, [vp, vp]),
     "e2sar_hip_total_hdr_len": (sz, [i]),
     "e2sar_hip_max_pld_len": (sz, [u32, i]),
     "e2sar_hip_num_packets": (sz, [sz, sz]),
@@ -136,6 +143,9 @@ SIGNATURES = {
     "e2sar_hip_reas_get_stats": (i, [vp, C.POINTER(ReasStats)]),
     "e2sar_hip_reas_recycle": (i, [vp, i, vp]),
     "e2sar_hip_reas_reset_stats": (i, [vp, vp]),
+    "e2sar_hip_reas_compact": (i, [vp, vp]),
+    "e2sar_hip_route_workspace_bytes": (sz, [u32, u32]),
+    "e2sar_hip_route_batch": (i, [vp, vp, u32, vp, u32, i, u32, u32, vp, vp, vp, vp, sz, vp]),
 }
 
 

@@ -51,7 +51,9 @@ struct e2sar_hip_reas {
     e2sar_hip_ctx *ctx = nullptr;
     e2sar_hip_reas_config cfg{};
     ReasDev dev{};
-    void *stateMem = nullptr;        // slots | ctl | completed | lost
+    ReasDev alt{};                   // second slots + arena (COMPACTABLE), same ctl/lists
+    void *stateMem = nullptr;        // slots | ctl | shards | completed | lost
+    void *altSlots = nullptr;
     std::mutex mu;
 };
 
@@ -168,6 +170,26 @@ int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes)
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (kind < 0 || kind > 2) return fail(E2SAR_HIP_ERR_PARAMETER, "kind must be 0 (H2D), 1 (D2H) or 2 (D2D)");
+    if (bytes == 0) return E2SAR_HIP_OK;
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    const hipMemcpyKind k = kind == 0 ? hipMemcpyHostToDevice : kind == 1 ? hipMemcpyDeviceToHost : hipMemcpyDeviceToDevice;
+    HIP_TRY(hipMemcpyAsync(dst, src, bytes, k, s));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_stream_sync(e2sar_hip_ctx *ctx, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(hipStreamSynchronize(stream ? static_cast<hipStream_t>(stream) : ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
 /* ---------------- geometry ---------------- */
 
 size_t e2sar_hip_total_hdr_len(int useIPv6)
@@ -273,6 +295,27 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->dev.queueCapacity = cfg->queueCapacity;
     r->dev.lostCapacity = cfg->lostCapacity;
     r->dev.withLB = cfg->withLBHeader ? 1 : 0;
+    r->alt = r->dev;
+    if (cfg->flags & E2SAR_HIP_REAS_COMPACTABLE) {
+        e = hipMalloc(&r->altSlots, slotsB);
+        if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->alt.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
+        if (e != hipSuccess) {
+            (void)hipFree(r->altSlots);
+            (void)hipFree(r->stateMem);
+            (void)hipFree(r->dev.arena);
+            delete r;
+            return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(alternate arena): ") + hipGetErrorString(e));
+        }
+        r->alt.slots = reinterpret_cast<ReasSlot *>(r->altSlots);
+        e = hipMemsetAsync(r->altSlots, 0, slotsB, ctx->stream);
+        if (e != hipSuccess) {
+            delete r;
+            return hip_fail(e, "alternate table init");
+        }
+    } else {
+        r->alt.slots = nullptr;
+        r->alt.arena = nullptr;
+    }
     e = hipMemsetAsync(r->stateMem, 0, total, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
@@ -290,6 +333,13 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     if (!r) return;
     (void)hipSetDevice(r->ctx->device);
     (void)hipStreamSynchronize(r->ctx->stream);
+    if (r->alt.slots) {
+        // the two tables/arenas may have been swapped: free whichever is not in stateMem
+        auto *base = static_cast<uint8_t *>(r->stateMem);
+        ReasSlot *inState = reinterpret_cast<ReasSlot *>(base);
+        (void)hipFree(r->dev.slots == inState ? static_cast<void *>(r->alt.slots) : static_cast<void *>(r->dev.slots));
+        (void)hipFree(r->alt.arena);
+    }
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
     delete r;
@@ -428,6 +478,24 @@ int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream)
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    if (!r->alt.slots) return fail(E2SAR_HIP_ERR_LOGIC, "reassembler was not created COMPACTABLE");
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    ReasCtl c;
+    HIP_TRY(hipStreamSynchronize(s));
+    HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+    if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
+    hipError_t e = launch_compact(r->dev, r->alt, s);
+    if (e != hipSuccess) return hip_fail(e, "compact launch");
+    std::swap(r->dev.slots, r->alt.slots);
+    std::swap(r->dev.arena, r->alt.arena);
+    return E2SAR_HIP_OK;
+}
+
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
 {
     if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
@@ -441,6 +509,30 @@ int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
     HIP_TRY(hipMemsetAsync(r->dev.shards, 0, sizeof(ReasShard) * kShards, s));
     HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, nCompleted), 0, 2 * sizeof(uint32_t), s));
     HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, errorFlags), 0, sizeof(uint32_t), s));
+    return E2SAR_HIP_OK;
+}
+
+size_t e2sar_hip_route_workspace_bytes(uint32_t nPackets, uint32_t world)
+{
+    return route_workspace_bytes(nPackets, world);
+}
+
+int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
+                          uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self, uint8_t *d_sendPackets,
+                          uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace, size_t workspaceBytes,
+                          void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (world == 0 || world > 64 || self >= world) return fail(E2SAR_HIP_ERR_PARAMETER, "world must be 1..64, self < world");
+    if ((stride & 15u) || stride < 48u) return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16, >= 48");
+    if (nPackets && (!d_packets || !d_lens || !d_sendPackets || !d_sendLens || !d_counts || !d_workspace))
+        return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (workspaceBytes < route_workspace_bytes(nPackets, world)) return fail(E2SAR_HIP_ERR_PARAMETER, "workspace too small");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = launch_route(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, d_sendPackets,
+                                d_sendLens, d_counts, d_workspace, s);
+    if (e != hipSuccess) return hip_fail(e, "route launch");
     return E2SAR_HIP_OK;
 }
 

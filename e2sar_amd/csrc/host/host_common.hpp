@@ -1,0 +1,39 @@
+// host_common.hpp -- internal helpers shared by the Segmenter/Reassembler façade.
+#pragma once
+
+#include <chrono>
+#include <map>
+#include <string>
+
+#include "e2sar_amd/e2sar.hpp"
+#include "e2sar_hip.h"
+
+namespace e2sar {
+namespace detail {
+
+bool read_ini(const std::string &path, std::map<std::string, std::string> &out, std::string &err);
+bool ini_bool(const std::map<std::string, std::string> &m, const std::string &k, bool def);
+double ini_num(const std::map<std::string, std::string> &m, const std::string &k, double def);
+
+// C-ABI status -> E2SARErrorInfo (status = -(E2SARErrorc))
+inline E2SARErrorInfo hip_error(int rc, const std::string &what)
+{
+    return E2SARErrorInfo{static_cast<E2SARErrorc>(-rc), what + ": " + e2sar_hip_last_error()};
+}
+
+inline uint64_t now_us()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::microseconds>(
+               std::chrono::system_clock::now().time_since_epoch())
+        .count();
+}
+
+inline uint64_t steady_ms()
+{
+    return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+}  // namespace detail
+}  // namespace e2sar

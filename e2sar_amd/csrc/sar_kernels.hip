@@ -692,6 +692,62 @@ __global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dro
     }
 }
 
+// Compaction: one block per slot of `from`.  Surviving (READY) events get a new buffer
+// at the bottom of the `to` arena and a slot in the (empty) `to` table; their partial
+// bytes are copied whole.  Nothing else touches either table during this launch, so the
+// insert needs only the CAS for slot ownership among compacting blocks.
+__global__ __launch_bounds__(kBlock) void reas_compact_kernel(ReasDev from, ReasDev to)
+{
+    __shared__ uint64_t sOff;
+    const ReasSlot *sl = from.slots + blockIdx.x;
+    if (sl->state != kReady) return;
+    const uint32_t bytes = sl->bytes;
+    if (threadIdx.x == 0) {
+        uint64_t off = kNoBuf;
+        if (sl->bufOff != kNoBuf) {
+            const uint64_t need = ((uint64_t)bytes + 255ull) & ~255ull;
+            off = atomicAdd(&to.ctl->compactTop, (unsigned long long)(need ? need : 256ull));
+            if (off + bytes > to.arenaBytes) {
+                off = kNoBuf;                      // cannot happen when to.arenaBytes >= from.arenaBytes
+                atomicOr(&to.ctl->errorFlags, 2u);
+            }
+        }
+        const uint32_t mask = to.tableSlots - 1u;
+        uint32_t h = slot_hash(sl->eventNum, sl->dataId, mask);
+        for (uint32_t probe = 0; probe < to.tableSlots; probe++, h = (h + 1u) & mask) {
+            if (atomicCAS(&to.slots[h].state, (uint32_t)kEmpty, (uint32_t)kBusy) == kEmpty) {
+                ReasSlot *d = to.slots + h;
+                d->dataId = sl->dataId;
+                d->bytes = bytes;
+                d->eventNum = sl->eventNum;
+                d->acc = sl->acc;
+                d->bufOff = off;
+                d->created = sl->created;
+                d->state = kReady;
+                atomicAdd(&to.ctl->compactUsed, 1u);
+                break;
+            }
+        }
+        sOff = off;
+    }
+    __syncthreads();
+    const uint64_t off = sOff;
+    if (off == kNoBuf || sl->bufOff == kNoBuf) return;
+    const uint8_t *src = from.arena + sl->bufOff;
+    uint8_t *dst = to.arena + off;
+    const uint32_t n16 = bytes >> 4;
+    for (uint32_t i = threadIdx.x; i < n16; i += kBlock) st16(dst + 16u * i, ld16(src + 16u * i));
+    for (uint32_t b = (n16 << 4) + threadIdx.x; b < bytes; b += kBlock) st1(dst + b, ld1(src + b));
+}
+
+__global__ void reas_compact_finish(ReasDev to)
+{
+    to.ctl->arenaTop = to.ctl->compactTop;
+    to.ctl->tableUsed = to.ctl->compactUsed;
+    to.ctl->compactTop = 0;
+    to.ctl->compactUsed = 0;
+}
+
 // ---------------------------------------------------------------------------------
 // launchers
 
@@ -744,6 +800,149 @@ hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stre
 {
     hipLaunchKernelGGL(reas_recycle_kernel, dim3(cdiv(R.tableSlots, kBlock)), dim3(kBlock), 0, stream,
                        R, dropCompleted ? 1 : 0);
+    return hipGetLastError();
+}
+
+hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t stream)
+{
+    hipError_t e = hipMemsetAsync(to.slots, 0, sizeof(ReasSlot) * (size_t)to.tableSlots, stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(reas_compact_kernel, dim3(from.tableSlots), dim3(kBlock), 0, stream, from, to);
+    hipLaunchKernelGGL(reas_compact_finish, dim3(1), dim3(1), 0, stream, to);
+    return hipGetLastError();
+}
+
+
+// ---------------------------------------------------------------------------------
+// multi-GPU: route a landed datagram batch to the rank that owns each event
+//
+// owner(eventNum) = eventNum % world.  Datagrams that cannot be parsed stay
+// on this rank (so their badHeaderDiscards are counted where they landed).  The packing
+// is stable: datagrams keep their landing order inside each destination's span, so an
+// in-order stream stays in order after the exchange.
+
+constexpr uint32_t kMaxWorld = 64;
+
+__device__ __forceinline__ uint32_t route_dest(const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                               uint32_t p, int withLB, uint32_t world, uint32_t self)
+{
+    const uint32_t hl = withLB ? kLBREHdrLen : kREHdrLen;
+    const uint32_t len = lens[p];
+    if (len < hl || len > stride) return self;
+    const uint8_t *re = pkts + (uint64_t)p * stride + (withLB ? kLBHdrLen : 0u);
+    const u32x4 w = ld16(re);
+    if (!re_valid(w.x)) return self;
+    const uint64_t ev = ((uint64_t)bswap32(w.w) << 32) | bswap32(ld4(re + 16));
+    return (uint32_t)(ev % world);
+}
+
+// per-block, per-destination counts (wave ballots, deterministic)
+__global__ __launch_bounds__(kBlock) void route_hist_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                            const uint32_t *__restrict__ lens, uint32_t n, int withLB,
+                                                            uint32_t world, uint32_t self,
+                                                            uint32_t *__restrict__ blockHist)
+{
+    __shared__ uint32_t cnt[kMaxWorld];
+    for (uint32_t d = threadIdx.x; d < world; d += kBlock) cnt[d] = 0;
+    __syncthreads();
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t dest = (p < n) ? route_dest(pkts, stride, lens, p, withLB, world, self) : 0xFFFFFFFFu;
+    for (uint32_t d = 0; d < world; d++) {
+        const uint64_t m = __ballot(dest == d);
+        if ((threadIdx.x & 63) == 0 && m) atomicAdd(&cnt[d], (uint32_t)__builtin_popcountll(m));
+    }
+    __syncthreads();
+    for (uint32_t d = threadIdx.x; d < world; d += kBlock) blockHist[(uint64_t)blockIdx.x * world + d] = cnt[d];
+}
+
+// one block: exclusive scans -> per-block bases, per-destination counts and bases
+__global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict__ blockHist, uint32_t nBlocks,
+                                                            uint32_t world, uint32_t *__restrict__ counts,
+                                                            uint32_t *__restrict__ destBase)
+{
+    __shared__ uint32_t tot[kMaxWorld];
+    for (uint32_t d = threadIdx.x; d < world; d += kBlock) {
+        uint32_t run = 0;
+        for (uint32_t b = 0; b < nBlocks; b++) {
+            const uint32_t c = blockHist[(uint64_t)b * world + d];
+            blockHist[(uint64_t)b * world + d] = run;
+            run += c;
+        }
+        tot[d] = run;
+        counts[d] = run;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t run = 0;
+        for (uint32_t d = 0; d < world; d++) {
+            destBase[d] = run;
+            run += tot[d];
+        }
+    }
+}
+
+// copy every datagram slot (stride bytes) to its place in the send buffer
+__global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                            const uint32_t *__restrict__ lens, uint32_t n, int withLB,
+                                                            uint32_t world, uint32_t self,
+                                                            const uint32_t *__restrict__ blockBase,
+                                                            const uint32_t *__restrict__ destBase,
+                                                            uint8_t *__restrict__ out, uint32_t *__restrict__ outLens)
+{
+    __shared__ uint32_t pos[kBlock];
+    __shared__ uint32_t waveCnt[kBlock / 64][kMaxWorld];
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t dest = (p < n) ? route_dest(pkts, stride, lens, p, withLB, world, self) : 0xFFFFFFFFu;
+    uint32_t rank = 0;
+    for (uint32_t d = 0; d < world; d++) {
+        const uint64_t m = __ballot(dest == d);
+        if (dest == d) rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) waveCnt[wv][d] = (uint32_t)__builtin_popcountll(m);
+    }
+    __syncthreads();
+    if (dest != 0xFFFFFFFFu) {
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wv; w++) before += waveCnt[w][dest];
+        const uint32_t q = destBase[dest] + blockBase[(uint64_t)blockIdx.x * world + dest] + before + rank;
+        pos[threadIdx.x] = q;
+        outLens[q] = lens[p];
+    }
+    __syncthreads();
+    const uint32_t p0 = blockIdx.x * kBlock;
+    const uint32_t np = (n - p0 < kBlock) ? n - p0 : kBlock;
+    const uint32_t spc = stride >> 4;
+    const uint32_t nch = np * spc;
+    const float rspc = 1.0f / (float)spc;
+    for (uint32_t i = threadIdx.x; i < nch; i += kBlock) {
+        uint32_t k = (uint32_t)((float)i * rspc);
+        if (k * spc > i) k--;
+        else if ((k + 1u) * spc <= i) k++;
+        const uint32_t c = i - k * spc;
+        st16(out + (uint64_t)pos[k] * stride + 16u * c, ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * c));
+    }
+}
+
+size_t route_workspace_bytes(uint32_t n, uint32_t world)
+{
+    const uint64_t nb = (n + kBlock - 1) / kBlock;
+    return (size_t)((nb * world + world) * sizeof(uint32_t));
+}
+
+hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
+                        uint32_t world, uint32_t self, uint8_t *out, uint32_t *outLens, uint32_t *counts,
+                        void *workspace, hipStream_t stream)
+{
+    if (world == 0 || world > kMaxWorld || self >= world) return hipErrorInvalidValue;
+    if (n == 0) return hipMemsetAsync(counts, 0, world * sizeof(uint32_t), stream);
+    const uint32_t nb = cdiv(n, kBlock);
+    uint32_t *blockHist = static_cast<uint32_t *>(workspace);
+    uint32_t *destBase = blockHist + (size_t)nb * world;
+    hipLaunchKernelGGL(route_hist_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
+                       self, blockHist);
+    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kBlock), 0, stream, blockHist, nb, world, counts, destBase);
+    hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
+                       self, blockHist, destBase, out, outLens);
     return hipGetLastError();
 }
 

@@ -38,7 +38,10 @@ struct ReasCtl {
     uint32_t nLost;
     uint32_t tableUsed;
     uint32_t errorFlags;
-    uint64_t pad[4];
+    unsigned long long compactTop;   // arena top of the destination arena during compaction
+    uint32_t compactUsed;            // slots claimed in the destination table
+    uint32_t pad0;
+    uint64_t pad[2];
 };
 
 // Per-packet counters are sharded (one 128-byte line per shard, shard = block % kShards)
@@ -84,5 +87,12 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
 hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);
 hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stream);
+// Move every in-progress event of `from` (slots + arena bytes) into the empty `to`
+// table/arena (same ctl), then make `to`'s top and slot count current.
+hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t stream);
+size_t route_workspace_bytes(uint32_t n, uint32_t world);
+hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
+                        uint32_t world, uint32_t self, uint8_t *out, uint32_t *outLens, uint32_t *counts,
+                        void *workspace, hipStream_t stream);
 
 }  // namespace e2sar_amd

@@ -1,0 +1,82 @@
+"""Multi-GPU SAR: events are owned by rank ``eventNum % world``.
+
+Normal operation needs no communication: each GPU segments and reassembles the events it
+owns.  When datagrams *land* on a rank that does not own their event (a modelled NIC /
+RSS spread), ``PacketRouter.route`` packs the landed batch into per-owner spans on the
+GPU (gfx950 route kernels behind e2sar_hip_route_batch) and ``exchange`` moves the spans
+with one all-to-all-v: counts first, then the datagram slots and their lengths.  With the
+``nccl`` backend (RCCL on ROCm) the transfer runs over xGMI, peer to peer, not as a ring.
+The reference never needs this step -- its load balancer steers every fragment of an
+event to one receiver (e2sarDPSegmenter.hpp:231-235) -- so there is no reference call
+pattern to mirror.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import List, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+
+def owner(event_num: int, world: int) -> int:
+    return int(event_num) % int(world)
+
+
+def exchange(send_pk: torch.Tensor, send_ln: torch.Tensor, counts: List[int], stride: int,
+             group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """All-to-all-v of datagram slots.
+
+    send_pk: uint8, sum(counts)*stride bytes, the span for rank d at offset
+    sum(counts[:d])*stride; send_ln: int32 lengths in the same order; counts: datagrams per
+    destination rank.  Returns (recv_pk, recv_ln, n_recv), spans ordered by source rank.
+    Works on any backend that implements all_to_all_single (nccl/RCCL on GPU, gloo on CPU).
+    """
+    world = dist.get_world_size(group)
+    if len(counts) != world:
+        raise ValueError("counts must have one entry per rank")
+    dev = send_pk.device
+    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
+    rcnt = torch.empty_like(cnt)
+    dist.all_to_all_single(rcnt, cnt, group=group)
+    rc = [int(x) for x in rcnt.tolist()]
+    n_recv = sum(rc)
+    recv_pk = torch.empty(max(n_recv, 1) * stride, dtype=torch.uint8, device=dev)
+    recv_ln = torch.empty(max(n_recv, 1), dtype=torch.int32, device=dev)
+    n_send = sum(counts)
+    dist.all_to_all_single(recv_pk[: n_recv * stride], send_pk[: n_send * stride],
+                           [c * stride for c in rc], [c * stride for c in counts], group=group)
+    dist.all_to_all_single(recv_ln[:n_recv], send_ln[:n_send], rc, list(counts), group=group)
+    return recv_pk, recv_ln, n_recv
+
+
+class PacketRouter:
+    """Packs a landed datagram batch into per-owner spans on the GPU."""
+
+    def __init__(self, ctx, stride: int, max_packets: int, world: int, rank: int, with_lb_header: bool = True):
+        from ._capi import lib
+        self.ctx = ctx
+        self.stride = stride
+        self.world = world
+        self.rank = rank
+        self.with_lb = with_lb_header
+        self.max_packets = max_packets
+        d = ctx.torch_device
+        self.send_pk = torch.empty(max(max_packets, 1) * stride, dtype=torch.uint8, device=d)
+        self.send_ln = torch.empty(max(max_packets, 1), dtype=torch.int32, device=d)
+        self.counts = torch.zeros(world, dtype=torch.int32, device=d)
+        ws = int(lib().e2sar_hip_route_workspace_bytes(max_packets, world))
+        self.workspace = torch.empty(max(ws, 16), dtype=torch.uint8, device=d)
+
+    def route(self, pk: torch.Tensor, ln: torch.Tensor, n: int, stream: Optional[torch.cuda.Stream] = None):
+        """Returns (send_pk, send_ln, counts) with counts still on the device."""
+        from ._capi import check, lib
+        from .sar import _stream_handle
+        if n > self.max_packets:
+            raise ValueError("batch larger than the router was sized for")
+        check(lib().e2sar_hip_route_batch(
+            self.ctx.handle, C.c_void_p(pk.data_ptr()), self.stride, C.c_void_p(ln.data_ptr()), n,
+            1 if self.with_lb else 0, self.world, self.rank, C.c_void_p(self.send_pk.data_ptr()),
+            C.c_void_p(self.send_ln.data_ptr()), C.c_void_p(self.counts.data_ptr()),
+            C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(_stream_handle(stream))))
+        return self.send_pk, self.send_ln, self.counts

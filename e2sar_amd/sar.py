@@ -153,10 +153,11 @@ class DeviceReassembler:
     """
 
     def __init__(self, ctx: Context, with_lb_header: bool = False, table_slots: int = 4096,
-                 queue_capacity: int = 4096, lost_capacity: int = 4096, arena_bytes: int = 1 << 30):
+                 queue_capacity: int = 4096, lost_capacity: int = 4096, arena_bytes: int = 1 << 30,
+                 compactable: bool = False):
         self.ctx = ctx
         cfg = _capi.ReasConfig(1 if with_lb_header else 0, table_slots, queue_capacity,
-                               lost_capacity, arena_bytes)
+                               lost_capacity, arena_bytes, _capi.REAS_COMPACTABLE if compactable else 0, 0)
         h = C.c_void_p()
         check(lib().e2sar_hip_reas_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self._h = h
@@ -210,6 +211,11 @@ class DeviceReassembler:
 
     def recycle(self, force: bool = False, stream: Optional[torch.cuda.Stream] = None) -> None:
         check(lib().e2sar_hip_reas_recycle(self._h, 1 if force else 0, C.c_void_p(_stream_handle(stream))))
+
+    def compact(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Move in-progress events to the alternate arena (see e2sar_hip_reas_compact)."""
+        check(lib().e2sar_hip_reas_compact(self._h, C.c_void_p(_stream_handle(stream))))
+        self.arena_ptr = int(lib().e2sar_hip_reas_arena(self._h) or 0)
 
     def reset_stats(self, stream: Optional[torch.cuda.Stream] = None) -> None:
         check(lib().e2sar_hip_reas_reset_stats(self._h, C.c_void_p(_stream_handle(stream))))

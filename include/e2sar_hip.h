@@ -71,6 +71,10 @@ int e2sar_hip_host_free(void *p);
 int e2sar_hip_memcpy_h2d(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
 int e2sar_hip_memcpy_d2h(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
 int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes);
+/* asynchronous copy on `stream` (NULL = context stream); kind 0 = H2D, 1 = D2H, 2 = D2D */
+int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind,
+                           void *stream);
+int e2sar_hip_stream_sync(e2sar_hip_ctx *ctx, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* geometry (e2sarHeaders.hpp:415-421, e2sarDPSegmenter.hpp:241, e2sarDPSegmenter.cpp:670) */
@@ -131,7 +135,13 @@ typedef struct e2sar_hip_reas_config {
     uint32_t queueCapacity;    /* completed-event records held until polled (QSIZE, hpp:126) */
     uint32_t lostCapacity;     /* lost-event records held until polled */
     uint64_t arenaBytes;       /* device arena that receives reassembled event bytes */
+    uint32_t flags;            /* E2SAR_HIP_REAS_* */
+    uint32_t reserved;
 } e2sar_hip_reas_config;
+
+/* Allocate a second table + arena so e2sar_hip_reas_compact() can move in-progress
+ * events out of a full arena (streaming use: events that straddle batches). */
+#define E2SAR_HIP_REAS_COMPACTABLE 1u
 
 /* Reassembled event handed to the caller (getEvent's out-params, cpp:626-641).
  * The bytes live at e2sar_hip_reas_arena() + arenaOffset until the arena is recycled. */
@@ -204,8 +214,31 @@ int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out);
  * promises it no longer reads event bytes from the arena.  `force` drops in-progress
  * events without logging them.  Asynchronous. */
 int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream);
+/* Streaming form of recycle: move every in-progress event (its table entry and the
+ * bytes received so far) to the alternate table/arena, which becomes current; the old
+ * arena is free again.  Needs E2SAR_HIP_REAS_COMPACTABLE, and every completed record
+ * polled (their arena offsets refer to the old arena; copy the bytes out first).
+ * Asynchronous; e2sar_hip_reas_arena() returns the new base afterwards. */
+int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream);
 /* Zero every counter and the lost/completion lists (asynchronous). */
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
+
+/* ------------------------------------------------------------------ */
+/* multi-GPU: events are owned by rank eventNum % world.  A rank that received       */
+/* (landed) datagrams of other ranks' events routes them: this packs the batch into */
+/* per-destination spans (stable order) and reports the span sizes, ready for one   */
+/* all-to-all-v over RCCL.  The reference never needs this step: its load balancer  */
+/* steers every fragment of an event to one receiver (e2sarDPSegmenter.hpp:231-235). */
+
+size_t e2sar_hip_route_workspace_bytes(uint32_t nPackets, uint32_t world);
+/* d_sendPackets: nPackets*stride bytes; d_sendLens: nPackets; d_counts: world entries
+ * (datagrams per destination rank).  Datagrams whose RE header does not parse stay on
+ * `self`.  world <= 64.  Asynchronous. */
+int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride,
+                          const uint32_t *d_lens, uint32_t nPackets, int withLBHeader,
+                          uint32_t world, uint32_t self, uint8_t *d_sendPackets,
+                          uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
+                          size_t workspaceBytes, void *stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,339 @@
+"""Reference-shaped data-plane tests through e2sar_py (C++ facade -> C ABI -> gfx950).
+
+Mirrors test/e2sar_seg_test.cpp (DPSegTest1-4), test/e2sar_reas_test.cpp (DPReasTest1-4)
+and test/py_test/test_b2b_DP.py: UDP loopback on 127.0.0.1, useCP off, the Reassembler
+expecting the LB header the missing load balancer would have stripped.  Datagrams
+captured on a plain socket are compared bit-for-bit with the oracle, taking the
+per-event LB tick and entropy (random by design in the reference) from the datagram.
+"""
+import socket
+import threading
+import time
+
+import numpy as np
+import pytest
+
+import oracle_ffi as O
+
+pytestmark = pytest.mark.gpu
+
+DP = "127.0.0.1"
+DATA_ID = 0x0505
+EVENTSRC_ID = 0x11223344
+SEND_STR = b"THIS IS A VERY LONG EVENT MESSAGE WE WANT TO SEND EVERY 1 SECONDS."   # 67 bytes
+_port = [21000]
+
+
+def next_port(span=1):
+    p = _port[0]
+    _port[0] += max(span, 8)
+    return p
+
+
+@pytest.fixture(scope="module")
+def E():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.fail("gpu test selected but no GPU is visible")
+    from e2sar_amd import e2sar_py
+    return e2sar_py
+
+
+def make_seg(E, port, mtu=1500, sockets=4, ver=2, rate=-1.0, data_id=DATA_ID):
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync=192.168.0.1:12345&data={DP}:{port}",
+                     E.EjfatURI.TokenType.instance)
+    f = E.DataPlane.Segmenter.SegmenterFlags()
+    f.useCP = False
+    f.mtu = mtu
+    f.numSendSockets = sockets
+    f.lbHdrVersion = ver
+    f.rateGbps = rate
+    return E.DataPlane.Segmenter(uri, data_id, EVENTSRC_ID, f)
+
+
+def make_reas(E, port, threads=1, with_lb=True, timeout_ms=500, port_range=-1):
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync=192.168.0.1:12345&data={DP}",
+                     E.EjfatURI.TokenType.instance)
+    f = E.DataPlane.Reassembler.ReassemblerFlags()
+    f.useCP = False
+    f.withLBHeader = with_lb
+    f.eventTimeout_ms = timeout_ms
+    f.portRange = port_range
+    f.rcvSocketBufSize = 4 * 1024 * 1024
+    f.arenaBytes = 256 << 20
+    return E.DataPlane.Reassembler(uri, E.IPAddress.from_string(DP), port, threads, f)
+
+
+def ok(res):
+    assert not res.has_error(), res.error()
+    assert res.value() == 0
+
+
+def capture(port, n, timeout=5.0):
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 8 << 20)
+    s.bind((DP, port))
+    s.settimeout(timeout)
+    out = []
+
+    def run():
+        try:
+            while len(out) < n:
+                out.append(s.recv(16384))
+        except socket.timeout:
+            pass
+        s.close()
+
+    t = threading.Thread(target=run)
+    t.start()
+    return t, out
+
+
+def check_against_oracle(dgrams, payloads, mtu, ver, data_id, first_evnum):
+    """Every captured datagram == the oracle's, with tick/entropy taken from the datagram."""
+    mp = O.max_pld_len(mtu)
+    by_ev = {}
+    for d in dgrams:
+        okv, did, off, blen, ev, _ = O.re_parse(d[16:36])
+        assert okv and did == data_id
+        by_ev.setdefault(ev, []).append(d)
+    assert sorted(by_ev) == list(range(first_evnum, first_evnum + len(payloads)))
+    for k, p in enumerate(payloads):
+        got = sorted(by_ev[first_evnum + k], key=lambda d: int.from_bytes(d[20:24], "big"))
+        tick = int.from_bytes(got[0][8:16], "big")
+        ent = int.from_bytes(got[0][6:8], "big")
+        pk, ln = O.segment_event(np.frombuffer(p, np.uint8), first_evnum + k, data_id, ent, tick, ver, mp)
+        assert len(got) == len(ln)
+        for j, d in enumerate(got):
+            assert d == pk[j, : int(ln[j])].tobytes(), f"event {k} datagram {j} differs"
+
+
+# ------------------------------- Segmenter ---------------------------------------
+
+@pytest.mark.parametrize("mtu,per_event", [(1500, 1), (104, 2)])
+def test_dpsegtest1_2_send_event(E, mtu, per_event):
+    # DPSegTest1 (msgCnt 5) / DPSegTest2-3 (MTU 104 -> msgCnt 10)
+    port = next_port()
+    t, got = capture(port, 5 * per_event)
+    seg = make_seg(E, port, mtu=mtu)
+    ok(seg.OpenAndStart())
+    assert seg.getSendStats().msgCnt == 0
+    for _ in range(5):
+        ok(seg.sendEvent(SEND_STR, len(SEND_STR)))
+    st = seg.getSendStats()
+    assert st.msgCnt == 5 * per_event and st.errCnt == 0
+    t.join()
+    seg.stopThreads()
+    assert len(got) == 5 * per_event
+    check_against_oracle(got, [SEND_STR] * 5, mtu, 2, DATA_ID, 0)
+
+
+def test_dpsegtest4_queue_callbacks_v3(E):
+    port = next_port()
+    t, got = capture(port, 10)
+    seg = make_seg(E, port, mtu=104, ver=3)
+    ok(seg.OpenAndStart())
+    fired = []
+    for i in range(5):
+        ok(seg.addToSendQueue(SEND_STR, len(SEND_STR), 0, 0, 0, lambda a: fired.append(a), i))
+    seg.stopThreads()            # drains the queue first (hpp:537-552)
+    t.join()
+    assert seg.getSendStats().msgCnt == 10
+    assert sorted(fired) == [0, 1, 2, 3, 4]
+    check_against_oracle(got, [SEND_STR] * 5, 104, 3, DATA_ID, 0)
+
+
+def test_event_numbering_and_overrides(E):
+    # sendEvent(_eventNum != 0) resets the counter (cpp:905-906); _dataId overrides (cpp:913)
+    port = next_port()
+    t, got = capture(port, 3)
+    seg = make_seg(E, port)
+    ok(seg.OpenAndStart())
+    ok(seg.sendEvent(SEND_STR, len(SEND_STR), 100, 0, 0))
+    ok(seg.sendEvent(SEND_STR, len(SEND_STR), 0, 77, 0x1234))
+    ok(seg.sendEvent(SEND_STR, len(SEND_STR)))
+    t.join()
+    seg.stopThreads()
+    evs = sorted((O.re_parse(d[16:36])[4], O.re_parse(d[16:36])[1], int.from_bytes(d[6:8], "big")) for d in got)
+    assert evs[0][:2] == (100, DATA_ID) and evs[1] == (101, 77, 0x1234) and evs[2][:2] == (102, DATA_ID)
+
+
+def test_segmenter_sanity_checks(E):
+    uri = E.EjfatURI(f"ejfat://u@1.2.3.4:1/lb/1?data={DP}:{next_port()}")
+    f = E.DataPlane.Segmenter.SegmenterFlags()
+    with pytest.raises(E.E2SARException):        # useCP without a sync address (hpp:306-307)
+        E.DataPlane.Segmenter(uri, 1, 2, f)
+    f.useCP = False
+    f.mtu = 9001
+    with pytest.raises(E.E2SARException):        # MTU > 9000 (hpp:310-311)
+        E.DataPlane.Segmenter(uri, 1, 2, f)
+    f.mtu = 64
+    with pytest.raises(E.E2SARException):        # MTU <= headers (hpp:315-316)
+        E.DataPlane.Segmenter(uri, 1, 2, f)
+    f.mtu = 1500
+    f.lbHdrVersion = 4
+    with pytest.raises(E.E2SARException):        # cpp:52-53
+        E.DataPlane.Segmenter(uri, 1, 2, f)
+
+
+# ------------------------------- Reassembler -------------------------------------
+
+@pytest.mark.parametrize("mtu,per_event", [(1500, 1), (80, 5)])
+def test_dpreastest1_2_loopback(E, mtu, per_event):
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port, mtu=mtu)
+    ok(seg.OpenAndStart())
+    for _ in range(5):
+        ok(seg.sendEvent(SEND_STR, len(SEND_STR)))
+    assert seg.getSendStats().msgCnt == 5 * per_event
+    got = []
+    for _ in range(5):
+        n, data, ev, did = reas.recvEventBytes(2000)
+        assert n == len(SEND_STR) and data == SEND_STR and did == DATA_ID
+        got.append(ev)
+    assert sorted(got) == [0, 1, 2, 3, 4]
+    st = reas.getStats()
+    assert st.eventSuccess == 5 and st.enqueueLoss == 0 and st.reassemblyLoss == 0
+    assert st.totalPackets == 5 * per_event and st.badHeaderDiscards == 0
+    assert reas.get_LostEvent() == ()
+    seg.stopThreads()
+    reas.stopThreads()
+
+
+def test_dpreastest3_port_ranges(E):
+    base = 19522
+    cases = [(1, -1, 0, (base, base)), (4, -1, 2, (base, base + 3)), (7, -1, 3, (base, base + 7)),
+             (1, 10, 10, (base, base + 1023)), (1, 1, 1, (base, base + 1))]
+    for threads, pr, want_pr, ports in cases:
+        r = make_reas(E, base, threads=threads, port_range=pr)
+        assert r.get_numRecvThreads() == threads
+        assert r.get_portRange() == want_pr
+        assert r.get_recvPorts() == ports
+        del r
+
+
+def test_dpreastest4_many_senders_fd_stats(E):
+    # 4 Segmenters -> 4 ports -> 1 receive thread; 20 events; per-port counts after stop
+    port = next_port(8)
+    reas = make_reas(E, port, threads=1, port_range=2)
+    ok(reas.OpenAndStart())
+    segs = [make_seg(E, port + i, data_id=DATA_ID + i) for i in range(4)]
+    for s in segs:
+        ok(s.OpenAndStart())
+    for k in range(5):
+        for s in segs:
+            ok(s.sendEvent(SEND_STR, len(SEND_STR)))
+    got = 0
+    while got < 20:
+        n, data, ev, did = reas.recvEventBytes(2000)
+        assert n == len(SEND_STR) and data == SEND_STR
+        got += 1
+    st = reas.getStats()
+    assert st.eventSuccess == 20 and st.enqueueLoss == 0 and st.reassemblyLoss == 0
+    assert reas.get_FDStats().has_error()          # only after the threads stop
+    for s in segs:
+        s.stopThreads()
+    reas.stopThreads()
+    fd = dict(reas.get_FDStats().value())
+    assert sorted(fd) == [port, port + 1, port + 2, port + 3] and all(v == 5 for v in fd.values())
+
+
+def test_lost_event_after_timeout(E):
+    # two of five fragments of event 9 never arrive: GC logs it (cpp:252-274, hpp:262-279)
+    port = next_port()
+    reas = make_reas(E, port, timeout_ms=200)
+    ok(reas.OpenAndStart())
+    mp = O.max_pld_len(80)
+    pk, ln = O.segment_event(np.frombuffer(SEND_STR, np.uint8), 9, 33, 5, 6, 2, mp)
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    for j in (0, 2, 4):
+        s.sendto(pk[j, : int(ln[j])].tobytes(), (DP, port))
+    s.sendto(b"\x00" * 40, (DP, port))             # bad RE header
+    deadline = time.time() + 5
+    lost = ()
+    while time.time() < deadline and lost == ():
+        time.sleep(0.1)
+        lost = reas.get_LostEvent()
+    assert lost == (9, 33, 3)
+    st = reas.getStats()
+    assert st.reassemblyLoss == 1 and st.eventSuccess == 0 and st.badHeaderDiscards == 1
+    assert st.totalPackets == 4
+    reas.stopThreads()
+
+
+# ------------------------------- back to back (test_b2b_DP.py) -------------------
+
+def test_b2b_send_bytes_recv_bytes(E):
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port)
+    ok(seg.OpenAndStart())
+    msg = SEND_STR[:65]
+    ok(seg.sendEvent(msg, len(msg)))
+    assert seg.getSendStats().msgCnt == 1
+    n, data, ev, did = reas.recvEventBytes(2000)
+    assert n == len(msg) and data == msg and did == DATA_ID
+    reas.stopThreads()
+    seg.stopThreads()
+
+
+def test_b2b_send_numpy_get_numpy(E):
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port, rate=2.0)
+    ok(seg.OpenAndStart())
+    arr = np.random.default_rng(1).random((100, 100, 50), dtype=np.float32)   # 2,000,000 bytes
+    ok(seg.sendNumpyArray(arr, arr.nbytes))
+    n, out, ev, did = reas.recv1DNumpyArray(np.float32().dtype, 5000)
+    assert n == arr.nbytes and did == DATA_ID
+    assert np.array_equal(arr.flatten(), out)
+    reas.stopThreads()
+    seg.stopThreads()
+
+
+def test_b2b_send_numpy_queue_get_numpy(E):
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port)
+    ok(seg.OpenAndStart())
+    rows = np.random.default_rng(2).integers(0, 256, (5, 100), dtype=np.uint8)
+    done = []
+    for i in range(5):
+        ok(seg.addNumpyArrayToSendQueue(rows[i], rows[i].nbytes, 0, 0, 0, lambda a: done.append(a), i))
+    recv = []
+    while len(recv) < 5:
+        n, out, ev, did = reas.recv1DNumpyArray(np.uint8().dtype, 3000)
+        assert n == 100
+        recv.append(out.tobytes())
+    seg.stopThreads()
+    assert sorted(done) == [0, 1, 2, 3, 4]
+    assert sorted(recv) == sorted(r.tobytes() for r in rows)      # order-insensitive (:251-256)
+    reas.stopThreads()
+
+
+def test_b2b_large_events_jumbo(E):
+    # 24 x 1 MiB at MTU 9000 through the socket path, paced so loopback does not drop
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port, mtu=9000, rate=4.0)
+    ok(seg.OpenAndStart())
+    rng = np.random.default_rng(3)
+    evs = [rng.integers(0, 256, 1 << 20, dtype=np.uint8) for _ in range(24)]
+    for e in evs:
+        ok(seg.addNumpyArrayToSendQueue(e, e.nbytes))
+    got = {}
+    while len(got) < 24:
+        n, out, ev, did = reas.recv1DNumpyArray(np.uint8().dtype, 10000)
+        assert n == 1 << 20, (n, reas.getStats().reassemblyLoss)
+        got[ev] = out
+    seg.stopThreads()
+    for k, e in enumerate(evs):
+        assert np.array_equal(got[k], e)
+    assert reas.getStats().eventSuccess == 24
+    reas.stopThreads()

@@ -334,3 +334,54 @@ def test_roundtrip_full_size(hip, mtu, size, n_ev, ver):
     R.recycle(force=False)
     R.reassemble(pk, seg.stride, ln, plan.total_packets)
     assert len(R.poll()) == n_ev
+
+
+def test_reas_compaction_keeps_partial_events(hip):
+    # streaming: events straddle two batches; completed records are polled, the arena is
+    # compacted, and the partial events finish in the new arena with the right bytes
+    torch = _torch()
+    from e2sar_amd import sar
+    evs, pk, ln = _events_stream(6, 50000, 1500, seed=71)
+    n, stride = pk.shape
+    st16 = (stride + 15) // 16 * 16
+    buf = np.zeros((n, st16), np.uint8)
+    buf[:, :stride] = pk
+    dpk = _dev(buf.reshape(-1), hip)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), hip)
+    R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=64, arena_bytes=1 << 20, compactable=True)
+    cut = n // 2 + 7                      # inside event 3
+    R.reassemble(dpk, st16, dln, cut)
+    first = {r.eventNum: R.event_bytes(r) for r in R.poll()}
+    before = R.stats()
+    assert before.inProgress == 1
+    R.compact()
+    R.reassemble(dpk[cut * st16:], st16, dln[cut:], n - cut)
+    second = {r.eventNum: R.event_bytes(r) for r in R.poll()}
+    got = {**first, **second}
+    assert sorted(got) == list(range(6))
+    for k, b in enumerate(evs):
+        assert got[k] == b.tobytes()
+    st = R.stats()
+    assert st.eventSuccess == 6 and st.inProgress == 0 and st.arenaUsed < before.arenaUsed + 3 * 50176
+
+
+@pytest.mark.parametrize("world,self_rank", [(2, 1), (8, 3)])
+def test_route_batch_matches_stable_route(hip, world, self_rank):
+    # gfx950 route kernels == the host restatement of the stable owner packing
+    from test_dist_gloo import stable_route
+    from e2sar_amd.dist import PacketRouter
+    evs, pk, ln = _events_stream(20, 7000, 1500, seed=81)
+    perm = np.random.default_rng(5).permutation(len(ln))      # arbitrary landing order
+    pk, ln = pk[perm].copy(), ln[perm].copy()
+    pk[3, 16] = 0x20                                          # one unparsable datagram stays home
+    n, stride = pk.shape
+    dpk = _dev(pk.reshape(-1), hip)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), hip)
+    router = PacketRouter(hip, stride, n, world, self_rank)
+    spk, sln, cnt = router.route(dpk, dln, n)
+    _torch().cuda.synchronize()
+    rpk, rln, rcounts = stable_route(pk, ln, world, self_rank)
+    assert cnt.cpu().tolist() == rcounts
+    np.testing.assert_array_equal(sln[:n].cpu().numpy().astype(np.uint32), rln)
+    got = spk[: n * stride].cpu().numpy().reshape(n, stride)
+    np.testing.assert_array_equal(got, rpk)

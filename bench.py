@@ -41,6 +41,8 @@ def parse():
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
     ap.add_argument("--roofline-steps", type=int, default=2)
+    ap.add_argument("--landing", choices=["own", "spread"], default="own",
+                    help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -116,7 +118,10 @@ def main():
     g.manual_seed(0xE25A2 + rank)
     ev_stride = (B + 255) // 256 * 256
     src = torch.randint(0, 256, (E, ev_stride), dtype=torch.uint8, device=dev, generator=g)
-    evnum = lambda i: i * world + rank          # owner rank = eventNum % world
+    if args.landing == "own":
+        evnum = lambda i: i * world + rank      # every local event is owned here: eventNum % world == rank
+    else:
+        evnum = lambda i: rank * E + i          # owners spread over all ranks: datagrams must be exchanged
     plans = []
     for b0 in range(0, E, args.batch_events):
         idx = range(b0, min(E, b0 + args.batch_events))
@@ -138,6 +143,19 @@ def main():
         segmentation of batch b+1 (double-buffered datagram slots)."""
         s0 = torch.cuda.current_stream()
         R.recycle(force=True)
+        if args.landing == "spread":
+            # datagrams land on this rank whatever their owner: route by owner on the GPU,
+            # one all-to-all-v over RCCL, reassemble what this rank owns
+            pk, ln = bufs[0]
+            for p in plans:
+                seg.segment(p, pk, ln)
+                spk, sln, cnt = router.route(pk, ln, p.total_packets)
+                if world > 1:
+                    rpk, rln, n = dexchange(spk, sln, [int(c) for c in cnt.tolist()], stride)
+                else:
+                    rpk, rln, n = spk, sln, p.total_packets
+                R.reassemble(rpk, stride, rln, n)
+            return
         if not args.overlap:
             pk, ln = bufs[0]
             for p in plans:
@@ -162,13 +180,46 @@ def main():
         s0.wait_stream(s1)
 
     side = torch.cuda.Stream() if args.overlap else None
+    router = None
+    if args.landing == "spread":
+        from e2sar_amd.dist import PacketRouter, exchange as dexchange
+        router = PacketRouter(ctx, stride, max_batch_pk, world, rank)
+        if args.overlap or not args.eager:
+            log(args, "landing=spread: counts are read back per batch -> eager, no overlap")
+        args.overlap = False
+        args.eager = True
 
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
     # ---- correctness gate (outside the timed region) ----
+    def verify_spread():
+        recs = R.poll()
+        st = R.stats()
+        arena = R.arena_tensor()
+        # per-event byte sums of every rank's source events, all-gathered
+        sums = src[:, :B].to(torch.int64).sum(dim=1)
+        ids = torch.tensor([evnum(i) for i in range(E)], dtype=torch.int64, device=dev)
+        table = torch.stack([ids, sums], dim=1)
+        if world > 1:
+            allt = [torch.empty_like(table) for _ in range(world)]
+            dist.all_gather(allt, table)
+            table = torch.cat(allt)
+        ref = {int(a): int(b) for a, b in table.tolist()}
+        owned = [e for e in ref if e % world == rank]
+        ok = (len(recs) == len(owned) and st.inProgress == 0 and st.badHeaderDiscards == 0)
+        for r in recs:
+            if not ok:
+                break
+            ok = int(arena[r.arenaOffset: r.arenaOffset + B].to(torch.int64).sum()) == ref.get(r.eventNum, -1)
+        if not ok:
+            raise SystemExit(f"rank {rank}: spread-landing verification FAILED ({len(recs)} records)")
+        return True
+
     def verify():
+        if args.landing == "spread":
+            return verify_spread()
         recs = R.poll()
         st = R.stats()
         arena = R.arena_tensor()
@@ -282,6 +333,7 @@ def main():
                 "parallelism": f"eventNum % {world} sharding (no collective)",
                 "launch": "eager" if args.eager else "hipGraph per step",
                 "overlap": bool(args.overlap),
+                "landing": args.landing,
                 "verified_roundtrip": verified,
             },
             "roofline": {

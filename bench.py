@@ -304,6 +304,25 @@ def main():
     dom, dom_ms = ("seg_kernel", seg_avg) if seg_avg >= reas_avg else ("reas_kernel", reas_avg)
     achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
 
+    # HBM traffic per launch of the dominant kernel, from the committed rocprofv3 PMC passes
+    # of this same workload (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
+    traffic = None
+    traffic_src = None
+    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    if os.path.exists(pmc_path):
+        try:
+            with open(pmc_path) as f:
+                pmc = json.load(f)
+            w = pmc.get("workload") or {}
+            if (w.get("mtu") == args.mtu and w.get("event_bytes") == B and w.get("batch_events") == args.batch_events
+                    and w.get("lb_version", 2) == args.lb_version):
+                for k, v in pmc["kernels"].items():
+                    if k.startswith(dom):
+                        traffic = int(v["hbm_bytes_per_launch"])
+                        traffic_src = pmc.get("file", "profiles/pmc_latest.json")
+        except (OSError, ValueError, KeyError):
+            traffic = None
+
     total_payload = E * B * world * K
     value = total_payload / elapsed / 2**30
     step_bytes = E * (4 * B + 72 * npk)
@@ -344,7 +363,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_unit": "bytes per launch (rocprofv3 PMC, committed)" if traffic else None,
+                "traffic_source": traffic_src,
                 "avg_launch_ms": {"seg_kernel": round(seg_avg, 5), "reas_kernel": round(reas_avg, 5)},
                 "algorithmic_bytes_per_launch": int(launch_bytes),
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),

@@ -33,12 +33,14 @@ def main():
     fd, wd, out = sys.argv[1:4]
     workload = None
     if "--workload" in sys.argv:
-        workload = sys.argv[sys.argv.index("--workload") + 1]
+        # e.g. mtu=1500,event_bytes=1048576,batch_events=128,lb_version=2
+        kv = sys.argv[sys.argv.index("--workload") + 1]
+        workload = {k: int(v) for k, v in (x.split("=") for x in kv.split(","))}
     fetch = load(fd, "FETCH_SIZE")
     write = load(wd, "WRITE_SIZE")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, --kernel-trace",
            "correction": "FETCH_SIZE x2 (gfx950 half-count on 16-B/lane streams), WRITE_SIZE x1, KiB -> bytes",
-           "workload": workload, "kernels": {}}
+           "workload": workload, "file": out, "kernels": {}}
     for k in sorted(set(fetch) | set(write)):
         f = fetch.get(k, [])
         w = write.get(k, [])

@@ -70,6 +70,84 @@ __global__ __launch_bounds__(256) void copyk(const uint8_t *__restrict__ src, ui
     }
 }
 
+// Datagram-pattern copies (no header work): packets of 1472 B (36 + 1436 payload).
+// MODE 10 "reas pattern": source-aligned 16-B loads of each packet slot, payload stored
+//   to event + k*1436 (dword-aligned 16-B stores, edge dwords stored singly) -- the store
+//   shape of reas_kernel.  MODE 11 "reas dst-aligned": destination-aligned chunks, the
+//   source read at a dword-aligned offset (edge dwords singly).
+template <int MODE>
+__global__ __launch_bounds__(256) void patk(const uint8_t *__restrict__ pk, uint8_t *__restrict__ ev, uint32_t npk)
+{
+    constexpr uint32_t S = 1472, H = 36, L = 1436, SPC = 92;
+    const uint32_t base = blockIdx.x * 1024 + threadIdx.x;
+    u32x4 x[4];
+    uint32_t ii[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t i = base + u * 256;
+        ii[u] = i;
+        const uint32_t p = i / SPC, c = i % SPC;
+        if (p >= npk) { x[u] = u32x4{0, 0, 0, 0}; continue; }
+        if (MODE == 10) {
+            x[u] = *(const G u32x4 *)(pk + (uint64_t)p * S + 16 * c);
+        } else {
+            const uint64_t d0 = (uint64_t)p * L;                 // dst offset of payload start
+            const uint64_t cb = (d0 & ~15ull) + 16ull * c;       // dst chunk
+            const int64_t so = (int64_t)cb - (int64_t)d0 + H;    // src offset within packet
+            const int64_t sc = so < 0 ? 0 : (so + 16 > S ? S - 16 : so);
+            x[u] = *(const G u32x4_a4 *)(pk + (uint64_t)p * S + sc);
+        }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint32_t i = ii[u];
+        const uint32_t p = i / SPC, c = i % SPC;
+        if (p >= npk) continue;
+        if (MODE == 10) {
+            const int32_t q0 = 16 * (int32_t)c;
+            uint8_t *dst = ev + (int64_t)p * L + q0 - H;
+            if (q0 >= (int32_t)H && q0 + 16 <= (int32_t)(H + L)) {
+                __builtin_nontemporal_store(x[u], (G u32x4_a4 *)dst);
+            } else {
+                for (int d = 0; d < 4; d++) {
+                    const int32_t q = q0 + 4 * d;
+                    if (q >= (int32_t)H && q + 4 <= (int32_t)(H + L)) *(G uint32_t *)(dst + 4 * d) = x[u][d];
+                }
+            }
+        } else {
+            const uint64_t d0 = (uint64_t)p * L, d1 = d0 + L;
+            const uint64_t cb = (d0 & ~15ull) + 16ull * c;
+            if (cb >= d1) continue;
+            if (cb >= d0 && cb + 16 <= d1) {
+                __builtin_nontemporal_store(x[u], (G u32x4 *)(ev + cb));
+            } else {
+                for (int d = 0; d < 4; d++) {
+                    const uint64_t a = cb + 4 * d;
+                    if (a >= d0 && a + 4 <= d1) *(G uint32_t *)(ev + a) = x[u][d];
+                }
+            }
+        }
+    }
+}
+
+template <int MODE>
+float runpat(const uint8_t *pk, uint8_t *ev, uint32_t npk, int iters)
+{
+    const uint32_t grid = (npk * 92 + 1023) / 1024;
+    hipEvent_t a, b;
+    CHECK(hipEventCreate(&a));
+    CHECK(hipEventCreate(&b));
+    patk<MODE><<<grid, 256>>>(pk, ev, npk);
+    CHECK(hipDeviceSynchronize());
+    CHECK(hipEventRecord(a));
+    for (int i = 0; i < iters; i++) patk<MODE><<<grid, 256>>>(pk, ev, npk);
+    CHECK(hipEventRecord(b));
+    CHECK(hipEventSynchronize(b));
+    float ms = 0;
+    CHECK(hipEventElapsedTime(&ms, a, b));
+    return (float)((double)npk * (1436 + 1472) * iters / (ms * 1e-3) / 1e9);
+}
+
 template <int MODE, int SH = 0>
 float run(const uint8_t *src, uint8_t *dst, uint64_t bytes, uint32_t shift, int iters)
 {
@@ -108,6 +186,9 @@ int main(int argc, char **argv)
     printf(", \"ld_pair_shift4\": %.1f", run<3, 4>(src, dst, bytes, 4, iters));
     printf(", \"ld_pair_shift5\": %.1f", run<3, 5>(src, dst, bytes, 5, iters));
     printf(", \"aligned_again\": %.1f", run<0>(src, dst, bytes, 0, iters));
+    const uint32_t npk = (uint32_t)(bytes / 1472);
+    printf(", \"pattern_reas_srcaligned\": %.1f", runpat<10>(src, dst, npk, iters));
+    printf(", \"pattern_reas_dstaligned\": %.1f", runpat<11>(src, dst, npk, iters));
     printf("}\n");
     return 0;
 }

@@ -41,6 +41,10 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
+    ap.add_argument("--reas", choices=["fused", "split", "pipelined"], default="pipelined",
+                    help="fused: one reassemble_batch launch per batch; split: classify + scatter launches "
+                         "in line; pipelined: one launch scatters batch b while other workgroups classify "
+                         "batch b+1 (two datagram buffers, one stream)")
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
@@ -129,14 +133,41 @@ def main():
         plans.append(seg.plan([(src[i].data_ptr(), B, evnum(i), 4321, 1 + (evnum(i) * 0x9E37) % 65535,
                                 (1 << 48) + evnum(i)) for i in idx]))
     max_batch_pk = max(p.total_packets for p in plans)
-    nbuf = 2 if args.overlap else 1
+    if args.reas == "pipelined" and args.overlap:
+        args.overlap = False                    # the pipeline is its own overlap
+    nbuf = 2 if (args.overlap or args.reas == "pipelined") else 1
     bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
     table = 1
     while table < 2 * E:
         table <<= 1
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096)
+    works = [R.alloc_work(max_batch_pk) for _ in range(nbuf)] if args.reas != "fused" else None
     torch.cuda.synchronize()
+
+    timing = []          # (kernel, start event, end event) while the roofline pass runs
+    timing_on = [False]
+
+    def timed(name, fn, *a, **kw):
+        """Launch fn; in the roofline pass bracket it with HIP events on the current stream."""
+        if not timing_on[0]:
+            return fn(*a, **kw)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = fn(*a, **kw)
+        e1.record()
+        timing.append((name, e0, e1))
+        return r
+
+    def reassemble(pk, ln, n, k, stream=None):
+        """The receive side of one batch: one fused launch, or classify + scatter."""
+        if args.reas == "fused":
+            timed("reas_kernel", R.reassemble, pk, stride, ln, n, stream=stream)
+        else:
+            w = works[k % nbuf]
+            timed("reas_classify_kernel", R.classify, pk, stride, ln, n, w, stream=stream)
+            timed("reas_scatter_kernel", R.scatter, pk, stride, n, w, stream=stream)
 
     def step():
         """One step: recycle the event table/arena, then segment -> reassemble every batch.
@@ -157,11 +188,28 @@ def main():
                     rpk, rln, n = spk, sln, p.total_packets
                 R.reassemble(rpk, stride, rln, n)
             return
+        if args.reas == "pipelined":
+            # seg(0), classify(0); then per batch: seg(b+1), [scatter(b) | classify(b+1)]
+            # in one launch; buffers b%2 are rewritten by seg(b+2) after that launch.
+            n0 = plans[0].total_packets
+            timed("seg_kernel", seg.segment, plans[0], *bufs[0])
+            timed("reas_classify_kernel", R.classify, bufs[0][0], stride, bufs[0][1], n0, works[0])
+            for k, p in enumerate(plans):
+                pk, ln = bufs[k % 2]
+                if k + 1 < len(plans):
+                    q = plans[k + 1]
+                    npk_, nln_ = bufs[(k + 1) % 2]
+                    timed("seg_kernel", seg.segment, q, npk_, nln_)
+                    timed("reas_scatter_classify_kernel", R.scatter_classify, stride, pk, p.total_packets,
+                          works[k % 2], npk_, nln_, q.total_packets, works[(k + 1) % 2])
+                else:
+                    timed("reas_scatter_kernel", R.scatter, pk, stride, p.total_packets, works[k % 2])
+            return
         if not args.overlap:
             pk, ln = bufs[0]
-            for p in plans:
-                seg.segment(p, pk, ln)
-                R.reassemble(pk, stride, ln, p.total_packets)
+            for k, p in enumerate(plans):
+                timed("seg_kernel", seg.segment, p, pk, ln)
+                reassemble(pk, ln, p.total_packets, k)
             return
         s1 = side
         s1.wait_stream(s0)
@@ -174,20 +222,22 @@ def main():
             ev = torch.cuda.Event()
             ev.record(s0)
             s1.wait_event(ev)
-            R.reassemble(pk, stride, ln, p.total_packets, stream=s1)
+            reassemble(pk, ln, p.total_packets, k, stream=s1)
             d = torch.cuda.Event()
             d.record(s1)
             done[k % nbuf] = d
         s0.wait_stream(s1)
 
     side = torch.cuda.Stream() if args.overlap else None
+
     router = None
     if args.landing == "spread":
         from e2sar_amd.dist import PacketRouter, exchange as dexchange
         router = PacketRouter(ctx, stride, max_batch_pk, world, rank)
-        if args.overlap or not args.eager:
-            log(args, "landing=spread: counts are read back per batch -> eager, no overlap")
+        if args.overlap or not args.eager or args.reas != "fused":
+            log(args, "landing=spread: counts are read back per batch -> eager, fused, no overlap")
         args.overlap = False
+        args.reas = "fused"
         args.eager = True
 
     for _ in range(args.warmup):
@@ -281,27 +331,30 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    # ---- per-kernel durations: HIP events around each launch, serialized, same stream ----
-    stream = torch.cuda.current_stream()
-    pk, ln = bufs[0]
-    seg_ms, reas_ms = [], []
-    for _ in range(args.roofline_steps):
-        R.recycle(force=True)
-        evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in plans]
-        for k, p in enumerate(plans):
-            evs[k][0].record(stream)
-            seg.segment(p, pk, ln)
-            evs[k][1].record(stream)
-            R.reassemble(pk, stride, ln, p.total_packets)
-            evs[k][2].record(stream)
-        torch.cuda.synchronize()
-        seg_ms += [e[0].elapsed_time(e[1]) for e in evs]
-        reas_ms += [e[1].elapsed_time(e[2]) for e in evs]
+    # ---- per-kernel durations: HIP events around each launch of the step, eager, on the
+    # stream the kernels run on (the step is single-stream unless --overlap) ----
+    was_overlap = args.overlap
+    args.overlap = False
+    timing_on[0] = True
+    for _ in range(max(1, args.roofline_steps)):
+        step()
+    torch.cuda.synchronize()
+    timing_on[0] = False
+    args.overlap = was_overlap
+    per = {}
+    for name, e0, e1 in timing:
+        per.setdefault(name, []).append(e0.elapsed_time(e1))
+    avg = {k: sum(v) / len(v) for k, v in per.items()}
     per_launch_events = sum(p.n_events for p in plans) / len(plans)
-    launch_bytes = per_launch_events * (2 * B + 36 * npk)   # seg: B + (B+36N); reas: (B+36N) + B
-    seg_avg = sum(seg_ms) / len(seg_ms)
-    reas_avg = sum(reas_ms) / len(reas_ms)
-    dom, dom_ms = ("seg_kernel", seg_avg) if seg_avg >= reas_avg else ("reas_kernel", reas_avg)
+    # algorithmic bytes of one launch of each bandwidth kernel:
+    #   seg: B + (B + 36N) per event; reassembly (fused, scatter, scatter+classify): (B + 36N) + B
+    #   (the classify share of scatter+classify -- 24 B of header/length read and 16 B of
+    #   record written per datagram -- is left out, so its rate is understated by ~1 %)
+    launch_bytes = per_launch_events * (2 * B + 36 * npk)
+    bw_kernels = [k for k in avg if k in ("seg_kernel", "reas_kernel", "reas_scatter_kernel",
+                                          "reas_scatter_classify_kernel")]
+    dom = max(bw_kernels, key=lambda k: sum(per[k]))      # most time in the step
+    dom_ms = avg[dom]
     achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
 
     # HBM traffic per launch of the dominant kernel, from the committed rocprofv3 PMC passes
@@ -353,6 +406,10 @@ def main():
                 "parallelism": f"eventNum % {world} sharding (no collective)",
                 "launch": "eager" if args.eager else "hipGraph per step",
                 "overlap": bool(args.overlap),
+                "reassembly": {"fused": "reas_kernel per batch",
+                               "split": "reas_classify_kernel + reas_scatter_kernel per batch",
+                               "pipelined": "reas_scatter_classify_kernel: scatter(b) beside classify(b+1), "
+                                            "2 datagram buffers"}[args.reas],
                 "landing": args.landing,
                 "verified_roundtrip": verified,
             },
@@ -366,7 +423,8 @@ def main():
                 "traffic": traffic,
                 "traffic_unit": "bytes per launch (rocprofv3 PMC, committed)" if traffic else None,
                 "traffic_source": traffic_src,
-                "avg_launch_ms": {"seg_kernel": round(seg_avg, 5), "reas_kernel": round(reas_avg, 5)},
+                "avg_launch_ms": {k: round(v, 5) for k, v in avg.items()},
+                "launches_per_step": {k: len(v) // max(1, args.roofline_steps) for k, v in per.items()},
                 "algorithmic_bytes_per_launch": int(launch_bytes),
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
             },

@@ -365,6 +365,81 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     return E2SAR_HIP_OK;
 }
 
+static int check_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride, uint32_t nPackets)
+{
+    const uint32_t hl = r->cfg.withLBHeader ? E2SAR_HIP_LBRE_HDR_LEN : E2SAR_HIP_RE_HDR_LEN;
+    if ((stride & 15u) || stride < hl + 16u) return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and > header + 16");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    if ((uint64_t)nPackets * (stride >> 4) > 0xFFFFFFFFull) return fail(E2SAR_HIP_ERR_OUT_OF_RANGE, "batch too large");
+    return E2SAR_HIP_OK;
+}
+
+size_t e2sar_hip_reas_work_bytes(uint32_t nPackets) { return work_bytes(nPackets); }
+
+int e2sar_hip_reas_classify(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                            const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
+                            void *d_work, size_t workBytes, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (nPackets == 0) return E2SAR_HIP_OK;
+    if (!d_packets || !d_lens || !d_work) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (((uintptr_t)d_work & 255u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer not 256-byte aligned");
+    if (workBytes < work_bytes(nPackets)) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer too small");
+    if (int st = check_batch(r, d_packets, stride, nPackets)) return st;
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, s);
+    if (e != hipSuccess) return hip_fail(e, "classify launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_scatter(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride, uint32_t nPackets,
+                           const void *d_work, size_t workBytes, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (nPackets == 0) return E2SAR_HIP_OK;
+    if (!d_packets || !d_work) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (((uintptr_t)d_work & 255u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer not 256-byte aligned");
+    if (workBytes < work_bytes(nPackets)) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer too small");
+    if (int st = check_batch(r, d_packets, stride, nPackets)) return st;
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, d_work, s);
+    if (e != hipSuccess) return hip_fail(e, "scatter launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const uint8_t *d_spk, uint32_t sn,
+                                    const void *d_swork, size_t sworkBytes, const uint8_t *d_cpk,
+                                    const uint32_t *d_clens, uint32_t cn, uint64_t now_ms, void *d_cwork,
+                                    size_t cworkBytes, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (sn == 0 && cn == 0) return E2SAR_HIP_OK;
+    if (sn) {
+        if (!d_spk || !d_swork) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer (scatter batch)");
+        if (((uintptr_t)d_swork & 255u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer not 256-byte aligned");
+        if (sworkBytes < work_bytes(sn)) return fail(E2SAR_HIP_ERR_PARAMETER, "scatter work buffer too small");
+        if (int st = check_batch(r, d_spk, stride, sn)) return st;
+    }
+    if (cn) {
+        if (!d_cpk || !d_clens || !d_cwork) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer (classify batch)");
+        if (((uintptr_t)d_cwork & 255u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "work buffer not 256-byte aligned");
+        if (cworkBytes < work_bytes(cn)) return fail(E2SAR_HIP_ERR_PARAMETER, "classify work buffer too small");
+        if (int st = check_batch(r, d_cpk, stride, cn)) return st;
+    }
+    if (sn && cn && d_swork == d_cwork) return fail(E2SAR_HIP_ERR_PARAMETER, "the two batches need different work buffers");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms,
+                                                d_cwork, s);
+    if (e != hipSuccess) return hip_fail(e, "scatter_classify launch");
+    return E2SAR_HIP_OK;
+}
+
 int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, void *stream)
 {
     if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
@@ -504,11 +579,12 @@ int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     // event counters live between arenaTop and inProgress; list counts after it
     auto *ctl = reinterpret_cast<uint8_t *>(r->dev.ctl);
-    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, eventSuccess), 0,
-                           offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, eventSuccess), s));
-    HIP_TRY(hipMemsetAsync(r->dev.shards, 0, sizeof(ReasShard) * kShards, s));
-    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, nCompleted), 0, 2 * sizeof(uint32_t), s));
-    HIP_TRY(hipMemsetAsync(ctl + offsetof(ReasCtl, errorFlags), 0, sizeof(uint32_t), s));
+    // kernels, not memset nodes: this call may be captured into a HIP graph
+    HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, eventSuccess),
+                              (offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, eventSuccess)) / 4, s));
+    HIP_TRY(launch_zero_words(r->dev.shards, sizeof(ReasShard) * kShards / 4, s));
+    HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, nCompleted), 2, s));
+    HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, errorFlags), 1, s));
     return E2SAR_HIP_OK;
 }
 

@@ -23,6 +23,12 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
+#ifndef E2SAR_REAS_EXPERIMENT_NOCLASSIFY
+#define E2SAR_REAS_EXPERIMENT_NOCLASSIFY 0
+#endif
+#ifndef E2SAR_REAS_U
+#define E2SAR_REAS_U 4
+#endif
 #ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
 #define E2SAR_REAS_CHUNKS_PER_BLOCK 4096u
 #endif
@@ -513,26 +519,24 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     return out;
 }
 
-// Completion (cpp:403-427): the run tail whose add brought curBytes to the event length.
-__device__ __forceinline__ void classify_finish(const ReasDev &R, const Classified &c)
+// Completion (cpp:403-427): erase from the table, count, and hand the event to the
+// completed queue (or record it lost when the queue is full or it had no buffer).
+__device__ void complete_event(const ReasDev &R, uint32_t slot, uint64_t ev, uint64_t boff, uint32_t bytes,
+                               uint32_t d, uint32_t frags)
 {
-    if (!c.tailAdd) return;
-    const uint64_t nb = (c.old & kAccBytesMask) + c.rb;
-    if (!(c.rc > 0 && nb == c.sbytes)) return;                // curBytes == bytes (cpp:403)
-    ReasSlot *sl = R.slots + c.slot;
+    ReasSlot *sl = R.slots + slot;
     st_agent(&sl->state, (uint32_t)kDone);                     // erase from the map (cpp:409)
     atomicAdd(&R.ctl->eventSuccess, 1ull);                     // cpp:426
     atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
-    const uint32_t frags = (uint32_t)(c.old >> kAccFragShift) + c.rc;
-    bool lostOnEnqueue = (c.boff == kNoBuf);
+    bool lostOnEnqueue = (boff == kNoBuf);
     if (!lostOnEnqueue) {
         const uint32_t idx = atomicAdd(&R.ctl->nCompleted, 1u);
         if (idx < R.queueCapacity) {
             e2sar_hip_event_rec rec;
-            rec.eventNum = c.ev;
-            rec.arenaOffset = c.boff;
-            rec.bytes = c.sbytes;
-            rec.dataId = (uint16_t)c.d;
+            rec.eventNum = ev;
+            rec.arenaOffset = boff;
+            rec.bytes = bytes;
+            rec.dataId = (uint16_t)d;
             rec.flags = 0;
             rec.numFragments = frags;
             rec.reserved = 0;
@@ -546,14 +550,28 @@ __device__ __forceinline__ void classify_finish(const ReasDev &R, const Classifi
         const uint32_t li = atomicAdd(&R.ctl->nLost, 1u);
         if (li < R.lostCapacity) {
             e2sar_hip_lost_rec lr;
-            lr.eventNum = c.ev;
+            lr.eventNum = ev;
             lr.numFragments = frags;
-            lr.dataId = (uint16_t)c.d;
+            lr.dataId = (uint16_t)d;
             lr.enqueueLoss = 1;
             lr.reserved = 0;
             R.lost[li] = lr;
         }
     }
+}
+
+// True when this run tail's add brought curBytes to the event length (cpp:403).
+__device__ __forceinline__ bool completes(const Classified &c)
+{
+    if (!c.tailAdd) return false;
+    const uint64_t nb = (c.old & kAccBytesMask) + c.rb;
+    return c.rc > 0 && nb == c.sbytes;
+}
+
+__device__ __forceinline__ void classify_finish(const ReasDev &R, const Classified &c)
+{
+    if (!completes(c)) return;
+    complete_event(R, c.slot, c.ev, c.boff, c.sbytes, c.d, (uint32_t)(c.old >> kAccFragShift) + c.rc);
 }
 
 // ---------------------------------------------------------------------------------
@@ -563,6 +581,43 @@ __device__ __noinline__ void store_bytes(uint8_t *dst, u32x4 v, uint32_t lo, uin
 {
     // bytes [lo, hi) of the 16-byte register chunk v to dst + (lo..hi); rare path
     for (uint32_t b = lo; b < hi; b++) st1(dst + b, (uint8_t)(v[b >> 2] >> (8u * (b & 3u))));
+}
+
+// Store the payload part of datagram chunk c (bytes [16c, 16c+16) of the slot) to its
+// place in the event: whole 16-byte stores inside the payload, whole dwords at the two
+// edges, bytes only for a sub-dword event tail or a non dword-congruent datagram.
+__device__ __forceinline__ void scatter_chunk(const PktInfo pi, uint32_t c, u32x4 v)
+{
+    if (pi.plen == 0) return;
+    // datagram bytes [16c, 16c+16) against the payload [hl, hl+plen)
+    const uint32_t q0 = 16u * c;
+    const uint32_t pend = pi.hl + pi.plen;
+    if (q0 >= pend || q0 + 16u <= pi.hl) return;
+    const uint32_t lo = (q0 < pi.hl) ? pi.hl - q0 : 0u;             // first chunk byte to keep
+    const uint32_t hi = (q0 + 16u <= pend) ? 16u : pend - q0;        // one past the last
+    uint8_t *dst = reinterpret_cast<uint8_t *>(pi.dst) + q0 - pi.hl;  // where chunk byte 0 goes
+    const bool congruent = ((pi.dst - pi.hl) & 3u) == 0;
+    if (lo == 0 && hi == 16u && congruent) {
+        st16u_nt(dst, v);
+    } else if (congruent) {
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++)
+            if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, v[d]);
+        const uint32_t t = hi & ~3u;                               // sub-dword event tail
+        if (t < hi && t >= lo) store_bytes(dst, v, t, hi);
+    } else {
+        store_bytes(dst, v, lo, hi);
+    }
+}
+
+__device__ __forceinline__ PktInfo ld_info(const PktInfo *p)
+{
+    const u32x4 v = *(const E2SAR_GLOBAL u32x4 *)(p);
+    PktInfo r;
+    r.dst = ((uint64_t)v.y << 32) | v.x;
+    r.plen = v.z;
+    r.hl = v.w;
+    return r;
 }
 
 // reas_kernel: one block = G consecutive datagrams, G*spc <= 256*U 16-byte chunks, so
@@ -577,7 +632,7 @@ __device__ __noinline__ void store_bytes(uint8_t *dst, u32x4 v, uint32_t lo, uin
 //      a sub-dword event tail or a datagram whose offset is not dword-congruent;
 //   5. the run tails complete events (their atomic results are consumed last).
 template <int U>
-__global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                       uint32_t stride, const uint32_t *__restrict__ lens,
                                                       uint32_t n, uint64_t now, uint32_t G)
 {
@@ -589,6 +644,152 @@ __global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *
 
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
+
+    const uint32_t spc = stride >> 4;
+    const uint32_t nch = gn * spc;
+    const float rspc = 1.0f / (float)spc;
+    const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
+    u32x4 x[U];
+    // chunk i -> (datagram, chunk within it); recomputed at store time rather than kept
+    // live across the classification (register pressure sets this kernel's occupancy)
+    auto split_chunk = [&](uint32_t i, uint32_t &p, uint32_t &c) {
+        const uint32_t ic = (i < nch) ? i : 0u;
+        p = (uint32_t)((float)ic * rspc);
+        if (p * spc > ic) p--;
+        else if ((p + 1u) * spc <= ic) p++;
+        c = ic - p * spc;
+    };
+    auto issue = [&](uint32_t r0) {
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            uint32_t p, c;
+            split_chunk(r0 + (uint32_t)u * kBlock + threadIdx.x, p, c);
+            x[u] = ld16(bpk + (uint64_t)p * stride + 16u * c);
+        }
+    };
+    issue(0);                          // round 0 is in flight while wave 0 classifies
+
+    // wave 0's run-tail state waits in LDS during the copy (only the atomic's return value
+    // stays in registers), which keeps the kernel at 8 waves per SIMD
+    __shared__ uint64_t sEv[64], sBoff[64];
+    __shared__ uint32_t sSlot[64], sBytes[64], sD[64], sRb[64], sRc[64], sTail[64];
+    unsigned long long old = 0;
+#if E2SAR_REAS_EXPERIMENT_NOCLASSIFY
+    // A/B experiment only (never shipped): destination straight from the header with no
+    // table, no atomics -- the pure-copy floor of this kernel's access pattern.
+    if (w0) {
+        const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
+        const uint32_t blen = bswap32(raw.re.z), off = bswap32(raw.re.y);
+        const uint64_t ev = ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4);
+        const uint64_t es = ((uint64_t)blen + 255ull) & ~255ull;
+        PktInfo pi;
+        pi.dst = (uint64_t)(R.arena + (ev & 127ull) * es + off);
+        pi.plen = lane < gn ? raw.len - hl : 0u;
+        pi.hl = hl;
+        sinfo[lane] = pi;
+    }
+#else
+    if (w0) {
+        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, blockIdx.x);
+        sinfo[lane] = cl.info;
+        old = cl.old;
+        sEv[lane] = cl.ev;
+        sBoff[lane] = cl.boff;
+        sSlot[lane] = cl.slot;
+        sBytes[lane] = cl.sbytes;
+        sD[lane] = cl.d;
+        sRb[lane] = cl.rb;
+        sRc[lane] = cl.rc;
+        sTail[lane] = cl.tailAdd ? 1u : 0u;
+    }
+#endif
+    __syncthreads();
+
+    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+        if (r0) issue(r0);
+#pragma unroll
+        for (int u = 0; u < U; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            if (i >= nch) continue;
+            uint32_t p, c;
+            split_chunk(i, p, c);
+            scatter_chunk(sinfo[p], c, x[u]);
+        }
+    }
+
+#if !E2SAR_REAS_EXPERIMENT_NOCLASSIFY
+    if (w0 && sTail[lane]) {
+        Classified cl;
+        cl.old = old;
+        cl.ev = sEv[lane];
+        cl.boff = sBoff[lane];
+        cl.slot = sSlot[lane];
+        cl.sbytes = sBytes[lane];
+        cl.d = sD[lane];
+        cl.rb = sRb[lane];
+        cl.rc = sRc[lane];
+        cl.tailAdd = true;
+        classify_finish(R, cl);
+    }
+#endif
+}
+
+// ---------------------------------------------------------------------------------
+// reassembly as two phases: classify (headers only, latency-bound) then scatter (bytes
+// only, bandwidth-bound).  Each phase is a launch of its own, or -- the pipelined form --
+// one launch scatters batch b while other workgroups of the same grid classify batch
+// b+1, so the table round trips of b+1 run under the copy of b instead of in front of it.
+//
+// Work buffer of a classified batch of n datagrams: PktInfo[n] then FinishRec[n].  A run
+// tail whose add completed its event sets kPktCompletes in its own PktInfo.hl and writes
+// FinishRec[p]; the scatter workgroup that owns datagram p publishes the event after its
+// own stores (the bytes of every workgroup are visible at the end of that launch).
+
+constexpr uint32_t kPktCompletes = 0x80000000u;
+
+// One wave: classify datagrams [p0, p0+64) of the batch.
+__device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const uint8_t *__restrict__ pkts,
+                                                      uint32_t stride, const uint32_t *__restrict__ lens,
+                                                      uint32_t n, uint64_t now, PktInfo *__restrict__ info,
+                                                      FinishRec *__restrict__ fin, uint32_t wave)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t p0 = wave * 64u;
+    if (p0 >= n) return;                                       // wave-uniform
+    const uint32_t gn = (n - p0 < 64u) ? n - p0 : 64u;
+    const RawHdr raw = load_hdr(R, pkts, stride, lens, p0 + ((lane < gn) ? lane : 0u));
+    const Classified cl = classify_wave(R, raw, stride, lane < gn, now, wave);
+    const bool done = completes(cl);
+    if (lane < gn) {
+        const u32x4 v = {(uint32_t)cl.info.dst, (uint32_t)(cl.info.dst >> 32), cl.info.plen,
+                         cl.info.hl | (done ? kPktCompletes : 0u)};
+        st16(reinterpret_cast<uint8_t *>(info + p0 + lane), v);
+    }
+    if (done) {
+        FinishRec f;
+        f.ev = cl.ev;
+        f.boff = cl.boff;
+        f.slot = cl.slot;
+        f.bytes = cl.sbytes;
+        f.frags = (uint32_t)(cl.old >> kAccFragShift) + cl.rc;
+        f.d = cl.d;
+        fin[p0 + lane] = f;
+    }
+}
+
+// One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
+template <int U>
+__device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                              uint32_t n, uint32_t G, const PktInfo *__restrict__ info,
+                                              const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
+{
+    const uint32_t g0 = blk * G;
+    const uint32_t gn = (n - g0 < G) ? n - g0 : G;
+    const uint32_t lane = threadIdx.x & 63u;
+
+    // every wave loads the records (cached) so no load result crosses a branch; they are
+    // issued before the payload loads so waiting for them does not wait for the payload
+    const PktInfo mine = ld_info(info + g0 + ((lane < gn) ? lane : 0u));
 
     const uint32_t spc = stride >> 4;
     const uint32_t nch = gn * spc;
@@ -609,12 +810,18 @@ __global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *
             x[u] = ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
         }
     };
-    issue(0);                          // round 0 is in flight while wave 0 classifies
-
-    Classified cl{};
-    if (w0) {
-        cl = classify_wave(R, raw, stride, lane < gn, now, blockIdx.x);
-        sinfo[lane] = cl.info;
+    issue(0);
+    bool fins = false;
+    if (threadIdx.x < 64) {
+        // a record that does not land inside the arena (a work buffer that was not filled
+        // by classify for this batch) is dropped and flagged, never written through
+        const uint64_t lo = (uint64_t)R.arena, hi = lo + R.arenaBytes;
+        const bool inside = mine.plen == 0 || (mine.dst >= lo && mine.dst + mine.plen <= hi);
+        if (lane < gn && !inside) atomicOr(&R.ctl->errorFlags, 8u);
+        PktInfo v = (lane < gn && inside) ? mine : PktInfo{0ull, 0u, 0u};
+        fins = (v.hl & kPktCompletes) != 0u;
+        v.hl &= ~kPktCompletes;
+        sinfo[lane] = v;
     }
     __syncthreads();
 
@@ -624,31 +831,61 @@ __global__ __launch_bounds__(kBlock) void reas_kernel(ReasDev R, const uint8_t *
         for (int u = 0; u < U; u++) {
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
             if (i >= nch) continue;
-            const PktInfo pi = sinfo[pp[u]];
-            if (pi.plen == 0) continue;
-            // datagram bytes [16c, 16c+16) against the payload [hl, hl+plen)
-            const uint32_t q0 = 16u * cc[u];
-            const uint32_t pend = pi.hl + pi.plen;
-            if (q0 >= pend || q0 + 16u <= pi.hl) continue;
-            const uint32_t lo = (q0 < pi.hl) ? pi.hl - q0 : 0u;             // first chunk byte to keep
-            const uint32_t hi = (q0 + 16u <= pend) ? 16u : pend - q0;        // one past the last
-            uint8_t *dst = reinterpret_cast<uint8_t *>(pi.dst) + q0 - pi.hl;  // where chunk byte 0 goes
-            const bool congruent = ((pi.dst - pi.hl) & 3u) == 0;
-            if (lo == 0 && hi == 16u && congruent) {
-                st16u_nt(dst, x[u]);
-            } else if (congruent) {
-#pragma unroll
-                for (uint32_t d = 0; d < 4; d++)
-                    if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, x[u][d]);
-                const uint32_t t = hi & ~3u;                               // sub-dword event tail
-                if (t < hi && t >= lo) store_bytes(dst, x[u], t, hi);
-            } else {
-                store_bytes(dst, x[u], lo, hi);
-            }
+            scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
         }
     }
 
-    if (w0) classify_finish(R, cl);
+    if (fins) {
+        const FinishRec f = fin[g0 + lane];
+        if (f.slot < R.tableSlots) complete_event(R, f.slot, f.ev, f.boff, f.bytes, f.d, f.frags);
+        else atomicOr(&R.ctl->errorFlags, 8u);
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+                                                               uint32_t stride, const uint32_t *__restrict__ lens,
+                                                               uint32_t n, uint64_t now, PktInfo *__restrict__ info,
+                                                               FinishRec *__restrict__ fin)
+{
+    classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+                                                              uint32_t stride, uint32_t n, uint32_t G,
+                                                              const PktInfo *__restrict__ info,
+                                                              const FinishRec *__restrict__ fin)
+{
+    __shared__ PktInfo sinfo[64];
+    scatter_group<U>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+}
+
+// Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
+// The classify workgroups have the low indices so they are dispatched first and their
+// round trips start while the scatter workgroups fill the machine.
+template <int U>
+__global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
+    ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
+    const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
+    const uint32_t *__restrict__ clens, uint32_t cn, uint64_t now, PktInfo *__restrict__ cinfo,
+    FinishRec *__restrict__ cfin, uint32_t nClsBlocks)
+{
+    __shared__ PktInfo sinfo[64];
+    if (blockIdx.x < nClsBlocks) {
+        classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
+                              blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+        return;
+    }
+    scatter_group<U>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+}
+
+// Zero nWords dwords.  Used instead of hipMemsetAsync wherever the launch may be captured
+// into a HIP graph: on this ROCm a captured 4-byte hipMemsetAsync node misbehaved when the
+// graph was replayed more than once (the next kernel faulted).
+__global__ __launch_bounds__(kBlock) void zero_words_kernel(uint32_t *p, uint64_t nWords)
+{
+    for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nWords; i += (uint64_t)gridDim.x * kBlock)
+        p[i] = 0u;
 }
 
 // ---------------------------------------------------------------------------------
@@ -753,6 +990,15 @@ __global__ void reas_compact_finish(ReasDev to)
 
 static inline uint32_t cdiv(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
 
+hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
+{
+    if (nWords == 0) return hipSuccess;
+    const uint64_t blocks = (nWords + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(zero_words_kernel, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0, stream,
+                       static_cast<uint32_t *>(p), nWords);
+    return hipGetLastError();
+}
+
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
@@ -774,18 +1020,64 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     return hipGetLastError();
 }
 
-hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
+static uint32_t scatter_group_size(uint32_t stride)
 {
-    constexpr int U = 4;
-    if (n == 0) return hipSuccess;
-    // datagrams per block: at most E2SAR_REAS_CHUNKS_PER_BLOCK 16-byte chunks (64 KiB), <= 64
-    // (tools/ab_chunks.sh: 2K-chunk blocks lose ~8 %, 1K-chunk blocks ~30 %, 4K-12K equal)
+    // datagrams per scatter workgroup: at most E2SAR_REAS_CHUNKS_PER_BLOCK 16-byte chunks, <= 64
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
     while (G > 1 && G * spc > E2SAR_REAS_CHUNKS_PER_BLOCK) G >>= 1;
+    return G;
+}
+
+hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (n == 0) return hipSuccess;
+    // (tools/ab_chunks.sh: 2K-chunk blocks lose ~8 %, 1K-chunk blocks ~30 %, 4K-12K equal)
+    const uint32_t G = scatter_group_size(stride);
     hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
                        now, G);
+    return hipGetLastError();
+}
+
+hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                uint32_t n, uint64_t now, void *work, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    uint8_t *w = static_cast<uint8_t *>(work);
+    hipLaunchKernelGGL(reas_classify_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens,
+                       n, now, reinterpret_cast<PktInfo *>(w), reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
+    return hipGetLastError();
+}
+
+hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
+                               const void *work, hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (n == 0) return hipSuccess;
+    const uint8_t *w = static_cast<const uint8_t *>(work);
+    const uint32_t G = scatter_group_size(stride);
+    hipLaunchKernelGGL((reas_scatter_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, n, G,
+                       reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
+    return hipGetLastError();
+}
+
+hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const uint8_t *spk, uint32_t sn,
+                                        const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
+                                        uint64_t now, void *cwork, hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream);
+    if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
+    const uint8_t *sw = static_cast<const uint8_t *>(swork);
+    uint8_t *cw = static_cast<uint8_t *>(cwork);
+    const uint32_t G = scatter_group_size(stride);
+    const uint32_t nCls = cdiv(cn, kBlock);
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), 0, stream, R, stride,
+                       spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
+                       reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
+                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
     return hipGetLastError();
 }
 
@@ -805,7 +1097,7 @@ hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stre
 
 hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t stream)
 {
-    hipError_t e = hipMemsetAsync(to.slots, 0, sizeof(ReasSlot) * (size_t)to.tableSlots, stream);
+    hipError_t e = launch_zero_words(to.slots, sizeof(ReasSlot) / 4 * (uint64_t)to.tableSlots, stream);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(reas_compact_kernel, dim3(from.tableSlots), dim3(kBlock), 0, stream, from, to);
     hipLaunchKernelGGL(reas_compact_finish, dim3(1), dim3(1), 0, stream, to);
@@ -934,7 +1226,7 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
                         void *workspace, hipStream_t stream)
 {
     if (world == 0 || world > kMaxWorld || self >= world) return hipErrorInvalidValue;
-    if (n == 0) return hipMemsetAsync(counts, 0, world * sizeof(uint32_t), stream);
+    if (n == 0) return launch_zero_words(counts, world, stream);
     const uint32_t nb = cdiv(n, kBlock);
     uint32_t *blockHist = static_cast<uint32_t *>(workspace);
     uint32_t *destBase = blockHist + (size_t)nb * world;

@@ -79,12 +79,37 @@ struct PktInfo {
 };
 static_assert(sizeof(PktInfo) == 16, "one dwordx4 per packet");
 
+// An event completed by a classified batch, published by the scatter kernel of that batch.
+struct FinishRec {
+    uint64_t ev;
+    uint64_t boff;
+    uint32_t slot;
+    uint32_t bytes;
+    uint32_t frags;
+    uint32_t d;
+};
+static_assert(sizeof(FinishRec) == 32, "two dwordx4 per record");
+
+// Work buffer of one classified batch of n datagrams (caller-owned, device memory):
+//   [0, 16n)                  PktInfo per datagram
+//   [work_fin_off(n), + 32n)  FinishRec per datagram (written only by completing run tails)
+inline size_t work_fin_off(uint32_t n) { return ((size_t)n * sizeof(PktInfo) + 255) & ~(size_t)255; }
+inline size_t work_bytes(uint32_t n) { return work_fin_off(n) + (size_t)n * sizeof(FinishRec); }
+
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream);
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
+hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                uint32_t n, uint64_t now, void *work, hipStream_t stream);
+hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
+                               const void *work, hipStream_t stream);
+hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const uint8_t *spk, uint32_t sn,
+                                        const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
+                                        uint64_t now, void *cwork, hipStream_t stream);
+hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream);   // p 4-byte aligned
 hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);
 hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stream);
 // Move every in-progress event of `from` (slots + arena bytes) into the empty `to`

@@ -181,6 +181,48 @@ class DeviceReassembler:
             self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
             int(now_ms), C.c_void_p(_stream_handle(stream))))
 
+    # ---- split form: classify (headers, table) then scatter (bytes), for pipelining ----
+    @staticmethod
+    def work_bytes(n: int) -> int:
+        return int(lib().e2sar_hip_reas_work_bytes(int(n)))
+
+    def alloc_work(self, n: int) -> torch.Tensor:
+        """Device work buffer for one classified batch of up to n datagrams."""
+        return torch.empty(self.work_bytes(n), dtype=torch.uint8, device=self.ctx.torch_device)
+
+    def classify(self, packets: torch.Tensor, stride: int, lens: torch.Tensor, n: int, work: torch.Tensor,
+                 now_ms: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:
+        if n == 0:
+            return
+        if lens.numel() < n or packets.numel() < n * stride:
+            raise ValueError("packet batch buffers too small")
+        check(lib().e2sar_hip_reas_classify(
+            self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n, int(now_ms),
+            C.c_void_p(work.data_ptr()), work.numel(), C.c_void_p(_stream_handle(stream))))
+
+    def scatter(self, packets: torch.Tensor, stride: int, n: int, work: torch.Tensor,
+                stream: Optional[torch.cuda.Stream] = None) -> None:
+        if n == 0:
+            return
+        if packets.numel() < n * stride:
+            raise ValueError("packet batch buffer too small")
+        check(lib().e2sar_hip_reas_scatter(
+            self._h, C.c_void_p(packets.data_ptr()), stride, n, C.c_void_p(work.data_ptr()), work.numel(),
+            C.c_void_p(_stream_handle(stream))))
+
+    def scatter_classify(self, stride: int, s_packets: torch.Tensor, s_n: int, s_work: torch.Tensor,
+                         c_packets: torch.Tensor, c_lens: torch.Tensor, c_n: int, c_work: torch.Tensor,
+                         now_ms: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """One launch: scatter classified batch b while classifying batch b+1."""
+        if s_n and s_packets.numel() < s_n * stride:
+            raise ValueError("scatter batch buffer too small")
+        if c_n and (c_lens.numel() < c_n or c_packets.numel() < c_n * stride):
+            raise ValueError("classify batch buffers too small")
+        check(lib().e2sar_hip_reas_scatter_classify(
+            self._h, stride, C.c_void_p(s_packets.data_ptr()), s_n, C.c_void_p(s_work.data_ptr()), s_work.numel(),
+            C.c_void_p(c_packets.data_ptr()), C.c_void_p(c_lens.data_ptr()), c_n, int(now_ms),
+            C.c_void_p(c_work.data_ptr()), c_work.numel(), C.c_void_p(_stream_handle(stream))))
+
     def gc(self, now_ms: int, timeout_ms: int, stream: Optional[torch.cuda.Stream] = None) -> None:
         check(lib().e2sar_hip_reas_gc(self._h, int(now_ms), int(timeout_ms), C.c_void_p(_stream_handle(stream))))
 

@@ -178,7 +178,8 @@ typedef struct e2sar_hip_reas_stats {
     uint64_t lostPending;
     uint64_t arenaUsed;
     uint64_t tableUsed;          /* slots ever claimed since the last recycle */
-    uint32_t errorFlags;         /* bit0 table full, bit1 arena full, bit2 probe timeout */
+    uint32_t errorFlags;         /* bit0 table full, bit1 arena full, bit2 probe timeout,
+                                    bit3 scatter record outside the arena (bad work buffer) */
     uint32_t reserved;
 } e2sar_hip_reas_stats;
 
@@ -195,6 +196,31 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
 int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
                                void *stream);
+
+/* The same work as e2sar_hip_reassemble_batch split in two phases so a caller can
+ * pipeline batches: classify (headers only: validate, look up / create, count) writes
+ * per-datagram destinations into d_work; scatter moves the payload bytes and publishes
+ * the events the batch completed.  Scatter a batch after its classify (same packets,
+ * stride, nPackets and work buffer, ordered on one stream or by an event); the work
+ * buffer is reusable once that scatter has run.  Batches are classified in arrival order.
+ * d_work: device memory, 256-byte aligned, e2sar_hip_reas_work_bytes(nPackets) bytes;
+ * no initialisation needed.  Asynchronous.  Replaces the same per-packet body
+ * (e2sarDPReassembler.cpp:335-427) as e2sar_hip_reassemble_batch. */
+size_t e2sar_hip_reas_work_bytes(uint32_t nPackets);
+int e2sar_hip_reas_classify(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                            const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
+                            void *d_work, size_t workBytes, void *stream);
+int e2sar_hip_reas_scatter(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                           uint32_t nPackets, const void *d_work, size_t workBytes, void *stream);
+/* Pipelined step, one launch: scatter the classified batch b (d_spk, sn, d_swork) while
+ * other workgroups of the same grid classify batch b+1 (d_cpk, d_clens, cn, d_cwork).
+ * The two batches use different packet and work buffers.  A stream of batches runs as
+ * classify(0), scatter_classify(0, 1), ..., scatter_classify(k-1, k), scatter(k). */
+int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride,
+                                    const uint8_t *d_spk, uint32_t sn, const void *d_swork,
+                                    size_t sworkBytes, const uint8_t *d_cpk,
+                                    const uint32_t *d_clens, uint32_t cn, uint64_t now_ms,
+                                    void *d_cwork, size_t cworkBytes, void *stream);
 
 /* GC pass: events whose first fragment is older than timeout_ms become lost
  * (reassemblyLoss, cpp:252-274).  Asynchronous. */

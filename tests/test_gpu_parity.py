@@ -146,8 +146,12 @@ def test_seg_generic_paths(hip):
 # reassembly parity
 
 
-def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096):
-    """Reassemble datagram rows pk[n, stride] (lens ln) on the GPU; returns ({(ev,d): bytes}, stats, reas)."""
+def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096, mode="fused"):
+    """Reassemble datagram rows pk[n, stride] (lens ln) on the GPU; returns ({(ev,d): bytes}, stats, reas).
+
+    mode "fused": one reassemble_batch per batch; "split": classify every batch (in
+    arrival order, one work buffer each) before any scatter -- the most decoupled order
+    the split API allows."""
     from e2sar_amd import sar
     torch = _torch()
     n, stride = pk.shape
@@ -158,9 +162,18 @@ def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096)
     dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), ctx)
     R = sar.DeviceReassembler(ctx, with_lb_header=with_lb, table_slots=table, arena_bytes=arena)
     cuts = np.linspace(0, n, batches + 1).astype(int)
-    for a, b in zip(cuts[:-1], cuts[1:]):
-        if b > a:
-            R.reassemble(dpk[a * st16:], st16, dln[a:], int(b - a), now_ms=now)
+    spans = [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
+    if mode == "fused":
+        for a, b in spans:
+            R.reassemble(dpk[a * st16:], st16, dln[a:], b - a, now_ms=now)
+    elif mode == "split":
+        works = [R.alloc_work(b - a) for a, b in spans]
+        for (a, b), w in zip(spans, works):
+            R.classify(dpk[a * st16:], st16, dln[a:], b - a, w, now_ms=now)
+        for (a, b), w in zip(spans, works):
+            R.scatter(dpk[a * st16:], st16, b - a, w)
+    else:
+        _pipelined(R, dpk, dln, st16, spans, now)
     torch.cuda.synchronize()
     got = {}
     for rec in R.poll():
@@ -168,6 +181,26 @@ def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096)
         assert key not in got
         got[key] = (R.event_bytes(rec), rec.numFragments)
     return got, R.stats(), R
+
+
+@pytest.fixture(params=["fused", "split", "pipelined"])
+def reas_mode(request):
+    return request.param
+
+
+def _pipelined(R, dpk, dln, stride, spans, now=0):
+    """classify(0), scatter_classify(0, 1), ..., scatter(last): two work buffers."""
+    works = [R.alloc_work(max(b - a for a, b in spans)) for _ in range(2)]
+    a0, b0 = spans[0]
+    R.classify(dpk[a0 * stride:], stride, dln[a0:], b0 - a0, works[0], now_ms=now)
+    for k in range(len(spans)):
+        a, b = spans[k]
+        if k + 1 < len(spans):
+            c, d = spans[k + 1]
+            R.scatter_classify(stride, dpk[a * stride:], b - a, works[k % 2],
+                               dpk[c * stride:], dln[c:], d - c, works[(k + 1) % 2], now_ms=now)
+        else:
+            R.scatter(dpk[a * stride:], stride, b - a, works[k % 2])
 
 
 def _reas_oracle(pk, ln, with_lb, qcap=100000):
@@ -204,26 +237,26 @@ def _check_reas(got, st, ref, rst):
 
 @pytest.mark.parametrize("mtu,size,n_ev", [(1500, 1 << 20, 8), (9000, 1 << 20, 8), (80, 67, 5),
                                            (1500, [1, 1436, 1437, 5000, 100000, 3], 6)])
-def test_reas_in_order_with_lb(hip, mtu, size, n_ev):
+def test_reas_in_order_with_lb(hip, mtu, size, n_ev, reas_mode):
     evs, pk, ln = _events_stream(n_ev, size, mtu)
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    got, st, _ = _reas_gpu(hip, pk, ln, True)
+    got, st, _ = _reas_gpu(hip, pk, ln, True, mode=reas_mode)
     _check_reas(got, st, ref, rst)
     for k, b in enumerate(evs):
         assert ref[(k, 4321)] == b.tobytes()
 
 
-def test_reas_without_lb_header(hip):
+def test_reas_without_lb_header(hip, reas_mode):
     evs, pk, ln = _events_stream(4, 50000, 1500)
     pk2 = np.zeros_like(pk)
     pk2[:, : pk.shape[1] - 16] = pk[:, 16:]
     ln2 = ln - 16
     ref, rst, _ = _reas_oracle(pk2, ln2, False)
-    got, st, _ = _reas_gpu(hip, pk2, ln2, False)
+    got, st, _ = _reas_gpu(hip, pk2, ln2, False, mode=reas_mode)
     _check_reas(got, st, ref, rst)
 
 
-def test_reas_interleaved_offset0_first(hip):
+def test_reas_interleaved_offset0_first(hip, reas_mode):
     # events interleaved and each event's tail fragments shuffled, offset-0 fragment first
     evs, pk, ln = _events_stream(6, 30000, 1500, seed=11)
     order = []
@@ -240,12 +273,12 @@ def test_reas_interleaved_offset0_first(hip):
     order = firsts + rest
     pk, ln = pk[order], ln[order]
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    for batches in (1, 3):
-        got, st, _ = _reas_gpu(hip, pk, ln, True, batches=batches)
+    for batches in (1, 3, 7):
+        got, st, _ = _reas_gpu(hip, pk, ln, True, batches=batches, mode=reas_mode)
         _check_reas(got, st, ref, rst)
 
 
-def test_reas_bad_and_short_datagrams(hip):
+def test_reas_bad_and_short_datagrams(hip, reas_mode):
     evs, pk, ln = _events_stream(5, 20000, 1500, seed=21)
     pk = pk.copy()
     ln = ln.copy()
@@ -253,7 +286,7 @@ def test_reas_bad_and_short_datagrams(hip):
     pk[9, 17] = 1             # reserved byte set -> invalid
     ln[12] = 30               # shorter than LB+RE headers
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    got, st, R = _reas_gpu(hip, pk, ln, True, now=100)
+    got, st, R = _reas_gpu(hip, pk, ln, True, now=100, mode=reas_mode)
     _check_reas(got, st, ref, rst)
     assert st.badHeaderDiscards == 3
     # incomplete events are reported lost by GC, with their fragment counts
@@ -271,32 +304,32 @@ def test_reas_bad_and_short_datagrams(hip):
     assert s2.reassemblyLoss == ro.stats()["reassemblyLoss"] and s2.inProgress == 0
 
 
-def test_reas_bounds_violation_counted(hip):
+def test_reas_bounds_violation_counted(hip, reas_mode):
     evs, pk, ln = _events_stream(2, 5000, 1500, seed=31)
     pk = pk.copy()
     # rewrite fragment 1's bufferOffset so it overruns the event (reference would overflow)
     pk[1, 20:24] = np.frombuffer((4990).to_bytes(4, "big"), np.uint8)
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    got, st, _ = _reas_gpu(hip, pk, ln, True)
+    got, st, _ = _reas_gpu(hip, pk, ln, True, mode=reas_mode)
     _check_reas(got, st, ref, rst)
     assert st.dataErrCnt == 1
 
 
-def test_reas_multiple_data_ids_same_event_numbers(hip):
+def test_reas_multiple_data_ids_same_event_numbers(hip, reas_mode):
     e1, p1, l1 = _events_stream(4, 9000, 1500, seed=41, data_id=1)
     e2, p2, l2 = _events_stream(4, 9000, 1500, seed=51, data_id=2)
     pk = np.concatenate([p1, p2])
     ln = np.concatenate([l1, l2])
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    got, st, _ = _reas_gpu(hip, pk, ln, True, table=64)
+    got, st, _ = _reas_gpu(hip, pk, ln, True, table=64, mode=reas_mode)
     _check_reas(got, st, ref, rst)
     assert len(got) == 8
 
 
-def test_reas_queue_and_arena_limits(hip):
+def test_reas_queue_and_arena_limits(hip, reas_mode):
     # arena too small for all events: the overflow is an enqueue loss, never a fault
     evs, pk, ln = _events_stream(6, 100000, 1500, seed=61)
-    got, st, R = _reas_gpu(hip, pk, ln, True, arena=3 * 100096)
+    got, st, R = _reas_gpu(hip, pk, ln, True, arena=3 * 100096, mode=reas_mode)
     assert st.eventSuccess == 6
     assert len(got) == 3 and st.enqueueLoss == 3
     assert st.errorFlags & 2
@@ -309,7 +342,7 @@ def test_reas_queue_and_arena_limits(hip):
 
 
 @pytest.mark.parametrize("mtu,size,n_ev,ver", [(1500, 1 << 20, 96, 2), (9000, 8 << 20, 12, 3)])
-def test_roundtrip_full_size(hip, mtu, size, n_ev, ver):
+def test_roundtrip_full_size(hip, mtu, size, n_ev, ver, reas_mode):
     torch = _torch()
     from e2sar_amd import sar
     g = torch.Generator(device=hip.torch_device)
@@ -320,7 +353,21 @@ def test_roundtrip_full_size(hip, mtu, size, n_ev, ver):
     pk, ln = seg.alloc_packets(plan.total_packets)
     seg.segment(plan, pk, ln)
     R = sar.DeviceReassembler(hip, with_lb_header=True, arena_bytes=n_ev * ((size + 255) // 256 * 256) + 4096)
-    R.reassemble(pk, seg.stride, ln, plan.total_packets)
+    work = R.alloc_work(plan.total_packets)
+
+    def reassemble():
+        n = plan.total_packets
+        if reas_mode == "fused":
+            R.reassemble(pk, seg.stride, ln, n)
+        elif reas_mode == "split":
+            R.classify(pk, seg.stride, ln, n, work)
+            R.scatter(pk, seg.stride, n, work)
+        else:
+            # four batches that cut through events, scatter of k beside classify of k+1
+            cuts = [0, n // 4 + 3, n // 2 + 11, 3 * n // 4 + 5, n]
+            _pipelined(R, pk, ln, seg.stride, list(zip(cuts[:-1], cuts[1:])))
+
+    reassemble()
     recs = R.poll()
     st = R.stats()
     assert st.eventSuccess == n_ev and len(recs) == n_ev and st.inProgress == 0
@@ -332,7 +379,7 @@ def test_roundtrip_full_size(hip, mtu, size, n_ev, ver):
         assert torch.equal(out, src[rec.eventNum]), f"event {rec.eventNum} differs"
     # recycle and go again: same results from a clean table
     R.recycle(force=False)
-    R.reassemble(pk, seg.stride, ln, plan.total_packets)
+    reassemble()
     assert len(R.poll()) == n_ev
 
 

@@ -41,7 +41,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
-    ap.add_argument("--reas", choices=["fused", "split", "pipelined"], default="pipelined",
+    ap.add_argument("--reas", choices=["fused", "split", "pipelined"], default="fused",
                     help="fused: one reassemble_batch launch per batch; split: classify + scatter launches "
                          "in line; pipelined: one launch scatters batch b while other workgroups classify "
                          "batch b+1 (two datagram buffers, one stream)")

@@ -26,6 +26,15 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_EXPERIMENT_NOCLASSIFY
 #define E2SAR_REAS_EXPERIMENT_NOCLASSIFY 0
 #endif
+// Occupancy cap of the fused reassembly kernel (0 = whatever its registers allow).
+#ifndef E2SAR_REAS_WAVES
+#define E2SAR_REAS_WAVES 0
+#endif
+#if E2SAR_REAS_WAVES
+#define E2SAR_REAS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(E2SAR_REAS_WAVES, E2SAR_REAS_WAVES)))
+#else
+#define E2SAR_REAS_WAVES_ATTR
+#endif
 #ifndef E2SAR_REAS_U
 #define E2SAR_REAS_U 4
 #endif
@@ -632,7 +641,7 @@ __device__ __forceinline__ PktInfo ld_info(const PktInfo *p)
 //      a sub-dword event tail or a datagram whose offset is not dword-congruent;
 //   5. the run tails complete events (their atomic results are consumed last).
 template <int U>
-__global__ __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(8, 8))) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                       uint32_t stride, const uint32_t *__restrict__ lens,
                                                       uint32_t n, uint64_t now, uint32_t G)
 {
@@ -1020,6 +1029,16 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     return hipGetLastError();
 }
 
+// Dynamic LDS requested only to cap workgroups per CU (A/B knob, default 0 = no cap):
+// fewer bytes in flight shorten the queueing latency that dependent table round trips see.
+static uint32_t occupancy_lds(const char *var)
+{
+    const char *v = getenv(var);
+    if (!v) return 0;
+    const long x = atol(v);
+    return (x > 0 && x <= 65536) ? (uint32_t)x : 0u;
+}
+
 static uint32_t scatter_group_size(uint32_t stride)
 {
     // datagrams per scatter workgroup: at most E2SAR_REAS_CHUNKS_PER_BLOCK 16-byte chunks, <= 64
@@ -1036,7 +1055,7 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
     if (n == 0) return hipSuccess;
     // (tools/ab_chunks.sh: 2K-chunk blocks lose ~8 %, 1K-chunk blocks ~30 %, 4K-12K equal)
     const uint32_t G = scatter_group_size(stride);
-    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
+    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_REAS_LDS"), stream, R, pkts, stride, lens, n,
                        now, G);
     return hipGetLastError();
 }
@@ -1058,7 +1077,7 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     const uint32_t G = scatter_group_size(stride);
-    hipLaunchKernelGGL((reas_scatter_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, n, G,
+    hipLaunchKernelGGL((reas_scatter_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
                        reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
@@ -1074,7 +1093,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     const uint32_t G = scatter_group_size(stride);
     const uint32_t nCls = cdiv(cn, kBlock);
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), 0, stream, R, stride,
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);

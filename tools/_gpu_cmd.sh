@@ -1,7 +1,7 @@
-mkdir -p gpurun_out/abr
-timeout -k 10 600 python -m pytest tests/test_gpu_parity.py -x -q > gpurun_out/abr/tests.log 2>&1 || { tail -30 gpurun_out/abr/tests.log; exit 1; }
-tail -2 gpurun_out/abr/tests.log
-for m in fused split; do
-  timeout -k 10 200 python bench.py --cpu-seconds 0 --reas $m > gpurun_out/abr/$m.json 2> gpurun_out/abr/$m.err || exit 1
+mkdir -p gpurun_out/abn
+for be in 72 80 88 96 104 112; do
+  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 30 --reas pipelined --batch-events $be > gpurun_out/abn/pipe_$be.json 2> gpurun_out/abn/pipe_$be.err || exit 1
 done
-timeout -k 10 200 python bench.py --cpu-seconds 0 --reas fused --batch-events 64 > gpurun_out/abr/fused64.json 2> gpurun_out/abr/fused64.err
+for be in 112 128; do
+  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 30 --reas fused --batch-events $be > gpurun_out/abn/fused_$be.json 2> gpurun_out/abn/fused_$be.err || exit 1
+done

@@ -180,13 +180,13 @@ def main():
             # one all-to-all-v over RCCL, reassemble what this rank owns
             pk, ln = bufs[0]
             for p in plans:
-                seg.segment(p, pk, ln)
-                spk, sln, cnt = router.route(pk, ln, p.total_packets)
+                timed("seg_kernel", seg.segment, p, pk, ln)
+                spk, sln, cnt = timed("route_kernels", router.route, pk, ln, p.total_packets)
                 if world > 1:
-                    rpk, rln, n = dexchange(spk, sln, [int(c) for c in cnt.tolist()], stride)
+                    rpk, rln, n = timed("exchange", dexchange, spk, sln, [int(c) for c in cnt.tolist()], stride)
                 else:
                     rpk, rln, n = spk, sln, p.total_packets
-                R.reassemble(rpk, stride, rln, n)
+                timed("reas_kernel", R.reassemble, rpk, stride, rln, n)
             return
         if args.reas == "pipelined":
             # seg(0), classify(0); then per batch: seg(b+1), [scatter(b) | classify(b+1)]

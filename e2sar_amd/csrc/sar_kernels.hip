@@ -39,7 +39,7 @@ constexpr int kBlock = 256;
 #define E2SAR_REAS_U 4
 #endif
 #ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
-#define E2SAR_REAS_CHUNKS_PER_BLOCK 4096u
+#define E2SAR_REAS_CHUNKS_PER_BLOCK 9216u
 #endif
 
 // Global-address-space accessors: the event/packet/arena pointers reach the kernels
@@ -1053,7 +1053,9 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
-    // (tools/ab_chunks.sh: 2K-chunk blocks lose ~8 %, 1K-chunk blocks ~30 %, 4K-12K equal)
+    // (A/B: at MTU 1500 2K-chunk blocks lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
+    // 8 MiB events 4K chunks (4 datagrams per block) lose 27 % to 9K-18K: per-event counter
+    // and table traffic grows with blocks per event)
     const uint32_t G = scatter_group_size(stride);
     hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_REAS_LDS"), stream, R, pkts, stride, lens, n,
                        now, G);

@@ -1,7 +1,6 @@
-mkdir -p gpurun_out/abn
-for be in 72 80 88 96 104 112; do
-  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 30 --reas pipelined --batch-events $be > gpurun_out/abn/pipe_$be.json 2> gpurun_out/abn/pipe_$be.err || exit 1
-done
-for be in 112 128; do
-  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 30 --reas fused --batch-events $be > gpurun_out/abn/fused_$be.json 2> gpurun_out/abn/fused_$be.err || exit 1
-done
+mkdir -p gpurun_out/cfg3
+tools/ab_variants.sh cfg3/a "--steps 30" base c4k c12k
+tools/ab_variants.sh cfg3/b "--steps 30 --mtu 9000" base c4k c12k
+tools/ab_variants.sh cfg3/c "--mtu 9000 --event-bytes 8388608 --events 280 --batch-events 16" base c4k c12k
+tools/ab_variants.sh cfg3/d "--mtu 9000 --event-bytes 8388608 --events 280 --batch-events 8" base
+tools/ab_variants.sh cfg3/e "--mtu 9000 --event-bytes 8388608 --events 280 --batch-events 32" base

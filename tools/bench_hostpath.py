@@ -4,8 +4,10 @@
 Receive direction: pinned host datagram batches (what recvmmsg fills) -> H2D -> reas_kernel
 -> completed events D2H into pinned host memory (what getEvent hands out).
 Send direction: pinned host events -> H2D -> seg_kernel -> datagrams D2H into pinned host
-memory (what sendmmsg drains).  Each direction double-buffers on its own copy/compute
-streams; --mode both runs the two directions at once (PCIe is full duplex).
+memory (what sendmmsg drains).  Each direction runs on two streams -- H2D copy + kernel on
+one, D2H copy on the other -- over --slots rotating buffer sets, so the whole process
+uses four streams (GPU_MAX_HW_QUEUES is 4: more streams than hardware queues share
+queues and serialise).  "both" runs the two directions at once (PCIe is full duplex).
 Prints one JSON line: payload GiB/s per direction and both-at-once, plus PCIe-only rates.
 """
 from __future__ import annotations
@@ -27,6 +29,7 @@ def main():
     ap.add_argument("--batch-events", type=int, default=32)
     ap.add_argument("--batches", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
+    ap.add_argument("--slots", type=int, default=3)
     args = ap.parse_args()
 
     import torch
@@ -44,7 +47,8 @@ def main():
     g = torch.Generator(device=dev)
     g.manual_seed(5)
     dev_events = torch.randint(0, 256, (BE, ev_stride), dtype=torch.uint8, device=dev, generator=g)
-    h_events = [torch.empty((BE, ev_stride), dtype=torch.uint8).pin_memory() for _ in range(2)]
+    S = args.slots
+    h_events = [torch.empty((BE, ev_stride), dtype=torch.uint8).pin_memory() for _ in range(S)]
     for h in h_events:
         h.copy_(dev_events)
     # build the datagram batch once on the device (any event numbers; each batch reuses them)
@@ -52,75 +56,67 @@ def main():
     pk0, ln0 = seg.alloc_packets(bpk)
     seg.segment(plan0, pk0, ln0)
     torch.cuda.synchronize()
-    h_pk = [torch.empty(bpk * stride, dtype=torch.uint8).pin_memory() for _ in range(2)]
-    h_ln = [torch.empty(bpk, dtype=torch.int32).pin_memory() for _ in range(2)]
+    h_pk = [torch.empty(bpk * stride, dtype=torch.uint8).pin_memory() for _ in range(S)]
+    h_ln = [torch.empty(bpk, dtype=torch.int32).pin_memory() for _ in range(S)]
     for a, b in zip(h_pk, h_ln):
         a.copy_(pk0[: bpk * stride])
         b.copy_(ln0[:bpk])
-    h_out_events = [torch.empty((BE, ev_stride), dtype=torch.uint8).pin_memory() for _ in range(2)]
-    h_out_pk = [torch.empty(bpk * stride, dtype=torch.uint8).pin_memory() for _ in range(2)]
+    h_out_events = [torch.empty((BE, ev_stride), dtype=torch.uint8).pin_memory() for _ in range(S)]
+    h_out_pk = [torch.empty(bpk * stride, dtype=torch.uint8).pin_memory() for _ in range(S)]
 
     # ---------------- device buffers ----------------
-    d_pk = [torch.empty(bpk * stride, dtype=torch.uint8, device=dev) for _ in range(2)]
-    d_ln = [torch.empty(bpk, dtype=torch.int32, device=dev) for _ in range(2)]
-    d_ev = [torch.empty((BE, ev_stride), dtype=torch.uint8, device=dev) for _ in range(2)]
-    d_spk = [seg.alloc_packets(bpk) for _ in range(2)]
-    plans = [seg.plan([(d_ev[s][i].data_ptr(), B, i, 4321, 1 + i, 7 + i) for i in range(BE)]) for s in range(2)]
+    d_pk = [torch.empty(bpk * stride, dtype=torch.uint8, device=dev) for _ in range(S)]
+    d_ln = [torch.empty(bpk, dtype=torch.int32, device=dev) for _ in range(S)]
+    d_ev = [torch.empty((BE, ev_stride), dtype=torch.uint8, device=dev) for _ in range(S)]
+    d_spk = [seg.alloc_packets(bpk) for _ in range(S)]
+    plans = [seg.plan([(d_ev[s][i].data_ptr(), B, i, 4321, 1 + i, 7 + i) for i in range(BE)]) for s in range(S)]
     # one reassembler per slot: a slot's arena is recycled only after its previous D2H finished
     R = [sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(64, 1 << (2 * BE).bit_length()),
-                               queue_capacity=4 * BE, arena_bytes=BE * ev_stride + 4096) for _ in range(2)]
+                               queue_capacity=4 * BE, arena_bytes=BE * ev_stride + 4096) for _ in range(S)]
     arena_views = [r.arena_tensor()[: BE * ev_stride] for r in R]   # built once (CAI import may sync)
-    rs = [torch.cuda.Stream() for _ in range(3)]      # recv: H2D, compute, D2H
-    ss = [torch.cuda.Stream() for _ in range(3)]      # send: H2D, compute, D2H
+    rs = [torch.cuda.Stream() for _ in range(2)]      # recv: H2D + kernel, D2H
+    ss = [torch.cuda.Stream() for _ in range(2)]      # send: H2D + kernel, D2H
 
     def recv_batch(k, ev_done):
-        s = k % 2
+        s = k % S
         with torch.cuda.stream(rs[0]):
             if ev_done[s] is not None:
                 rs[0].wait_event(ev_done[s])
             d_pk[s].copy_(h_pk[s], non_blocking=True)
             d_ln[s].copy_(h_ln[s], non_blocking=True)
+            R[s].recycle(force=True, stream=rs[0])    # events of this batch fill arena[0, BE*ev_stride)
+            R[s].reassemble(d_pk[s], stride, d_ln[s], bpk, stream=rs[0])
             e1 = torch.cuda.Event()
             e1.record(rs[0])
         rs[1].wait_event(e1)
         with torch.cuda.stream(rs[1]):
-            R[s].recycle(force=True, stream=rs[1])    # events of this batch fill arena[0, BE*ev_stride)
-            R[s].reassemble(d_pk[s], stride, d_ln[s], bpk, stream=rs[1])
-            e2 = torch.cuda.Event()
-            e2.record(rs[1])
-        rs[2].wait_event(e2)
-        with torch.cuda.stream(rs[2]):
             # the batch's events fill the recycled arena contiguously (256-B aligned buffers)
             h_out_events[s].view(-1).copy_(arena_views[s], non_blocking=True)
-            e3 = torch.cuda.Event()
-            e3.record(rs[2])
-        ev_done[s] = e3
+            e2 = torch.cuda.Event()
+            e2.record(rs[1])
+        ev_done[s] = e2
 
     def send_batch(k, ev_done):
-        s = k % 2
+        s = k % S
         with torch.cuda.stream(ss[0]):
             if ev_done[s] is not None:
                 ss[0].wait_event(ev_done[s])
             d_ev[s].copy_(h_events[s], non_blocking=True)
+            seg.segment(plans[s], d_spk[s][0], d_spk[s][1], stream=ss[0])
             e1 = torch.cuda.Event()
             e1.record(ss[0])
         ss[1].wait_event(e1)
         with torch.cuda.stream(ss[1]):
-            seg.segment(plans[s], d_spk[s][0], d_spk[s][1], stream=ss[1])
+            h_out_pk[s].copy_(d_spk[s][0][: bpk * stride], non_blocking=True)
             e2 = torch.cuda.Event()
             e2.record(ss[1])
-        ss[2].wait_event(e2)
-        with torch.cuda.stream(ss[2]):
-            h_out_pk[s].copy_(d_spk[s][0][: bpk * stride], non_blocking=True)
-            e3 = torch.cuda.Event()
-            e3.record(ss[2])
-        ev_done[s] = e3
+        ev_done[s] = e2
 
     def run(mode):
         best = 0.0
         for _ in range(args.iters):
             torch.cuda.synchronize()
-            rd, sd = [None, None], [None, None]
+            rd, sd = [None] * S, [None] * S
             t0 = time.perf_counter()
             for k in range(args.batches):
                 if mode in ("recv", "both"):
@@ -133,7 +129,7 @@ def main():
         return best
 
     # correctness of the recv direction: the reassembled batch equals the source events
-    rd = [None, None]
+    rd = [None] * S
     recv_batch(0, rd)
     torch.cuda.synchronize()
     recs = R[0].poll()
@@ -143,19 +139,19 @@ def main():
         assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], dev_events[r.eventNum, :B])
 
     res = {"config": f"host path: {BE} x {B} B events per batch, MTU {args.mtu}, pinned buffers, "
-                     f"3 streams per direction, double-buffered",
+                     f"2 streams per direction (H2D+kernel, D2H), {S} rotating buffer sets",
            "recv_GiBps": round(run("recv"), 2), "send_GiBps": round(run("send"), 2),
            "both_GiBps_each_direction": round(run("both"), 2)}
     # PCIe alone: the same copies without kernels
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(args.batches):
-        d_pk[k % 2].copy_(h_pk[k % 2], non_blocking=True)
+        d_pk[k % S].copy_(h_pk[k % S], non_blocking=True)
     torch.cuda.synchronize()
     res["pcie_h2d_GBps"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
     t0 = time.perf_counter()
     for k in range(args.batches):
-        h_out_pk[k % 2].copy_(d_spk[k % 2][0][: bpk * stride], non_blocking=True)
+        h_out_pk[k % S].copy_(d_spk[k % S][0][: bpk * stride], non_blocking=True)
     torch.cuda.synchronize()
     res["pcie_d2h_GBps"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
     print(json.dumps(res), flush=True)

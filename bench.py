@@ -372,7 +372,7 @@ def main():
                 for k, v in pmc["kernels"].items():
                     if k.startswith(dom):
                         traffic = int(v["hbm_bytes_per_launch"])
-                        traffic_src = pmc.get("file", "profiles/pmc_latest.json")
+                        traffic_src = pmc.get("file", "profiles/round1/final/pmc_summary.json")
         except (OSError, ValueError, KeyError):
             traffic = None
 

@@ -154,6 +154,16 @@ def main():
         h_out_pk[k % S].copy_(d_spk[k % S][0][: bpk * stride], non_blocking=True)
     torch.cuda.synchronize()
     res["pcie_d2h_GBps"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
+    # both directions at once, copies only, one stream per direction
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.batches):
+        with torch.cuda.stream(rs[0]):
+            d_pk[k % S].copy_(h_pk[k % S], non_blocking=True)
+        with torch.cuda.stream(rs[1]):
+            h_out_pk[k % S].copy_(d_spk[k % S][0][: bpk * stride], non_blocking=True)
+    torch.cuda.synchronize()
+    res["pcie_bidir_GBps_each"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
     print(json.dumps(res), flush=True)
 
 

@@ -1168,21 +1168,42 @@ __global__ __launch_bounds__(kBlock) void route_hist_kernel(const uint8_t *__res
     for (uint32_t d = threadIdx.x; d < world; d += kBlock) blockHist[(uint64_t)blockIdx.x * world + d] = cnt[d];
 }
 
-// one block: exclusive scans -> per-block bases, per-destination counts and bases
+// one block: exclusive scans -> per-block bases, per-destination counts and bases.
+// For each destination the nBlocks counts are scanned 256 at a time (wave prefix sums
+// through LDS, a running carry between tiles), so the scan costs nBlocks/256 block steps
+// per destination instead of nBlocks dependent loads.
 __global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict__ blockHist, uint32_t nBlocks,
                                                             uint32_t world, uint32_t *__restrict__ counts,
                                                             uint32_t *__restrict__ destBase)
 {
+    __shared__ uint32_t waveSum[kBlock / 64];
     __shared__ uint32_t tot[kMaxWorld];
-    for (uint32_t d = threadIdx.x; d < world; d += kBlock) {
-        uint32_t run = 0;
-        for (uint32_t b = 0; b < nBlocks; b++) {
-            const uint32_t c = blockHist[(uint64_t)b * world + d];
-            blockHist[(uint64_t)b * world + d] = run;
-            run += c;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    for (uint32_t d = 0; d < world; d++) {
+        uint32_t carry = 0;
+        for (uint32_t b0 = 0; b0 < nBlocks; b0 += kBlock) {
+            const uint32_t b = b0 + threadIdx.x;
+            const uint32_t c = (b < nBlocks) ? blockHist[(uint64_t)b * world + d] : 0u;
+            uint32_t inc = c;                                 // inclusive scan in the wave
+#pragma unroll
+            for (uint32_t o = 1; o < 64; o <<= 1) {
+                const uint32_t y = __shfl_up(inc, o);
+                if (lane >= o) inc += y;
+            }
+            if (lane == 63) waveSum[wv] = inc;
+            __syncthreads();
+            uint32_t before = carry;
+            for (uint32_t w = 0; w < wv; w++) before += waveSum[w];
+            if (b < nBlocks) blockHist[(uint64_t)b * world + d] = before + inc - c;
+            uint32_t tile = 0;
+            for (uint32_t w = 0; w < kBlock / 64; w++) tile += waveSum[w];
+            carry += tile;
+            __syncthreads();
         }
-        tot[d] = run;
-        counts[d] = run;
+        if (threadIdx.x == 0) {
+            tot[d] = carry;
+            counts[d] = carry;
+        }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1227,12 +1248,27 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
     const uint32_t spc = stride >> 4;
     const uint32_t nch = np * spc;
     const float rspc = 1.0f / (float)spc;
-    for (uint32_t i = threadIdx.x; i < nch; i += kBlock) {
-        uint32_t k = (uint32_t)((float)i * rspc);
-        if (k * spc > i) k--;
-        else if ((k + 1u) * spc <= i) k++;
-        const uint32_t c = i - k * spc;
-        st16(out + (uint64_t)pos[k] * stride + 16u * c, ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * c));
+    // two-phase rounds of 4 chunks per thread: 4 loads in flight before the stores
+    constexpr int UR = 4;
+    for (uint32_t r0 = 0; r0 < nch; r0 += kBlock * UR) {
+        u32x4 x[UR];
+        uint32_t kk[UR], cc[UR];
+#pragma unroll
+        for (int u = 0; u < UR; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            const uint32_t ic = (i < nch) ? i : 0u;
+            uint32_t k = (uint32_t)((float)ic * rspc);
+            if (k * spc > ic) k--;
+            else if ((k + 1u) * spc <= ic) k++;
+            kk[u] = k;
+            cc[u] = ic - k * spc;
+            x[u] = ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UR; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            if (i < nch) st16(out + (uint64_t)pos[kk[u]] * stride + 16u * cc[u], x[u]);
+        }
     }
 }
 

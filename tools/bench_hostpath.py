@@ -19,6 +19,11 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# D2H copies into pinned memory run as blit kernels on the compute queues.  With the
+# default 4 hardware queues per process, the four pipeline streams + the default stream
+# share queues, and a D2H blit queued behind the next batch's kernel serialises the
+# pipeline (send ran at half the PCIe rate).  8 queues give every stream its own.
+os.environ["GPU_MAX_HW_QUEUES"] = "8"   # the box exports 4
 sys.path.insert(0, ROOT)
 
 
@@ -30,6 +35,8 @@ def main():
     ap.add_argument("--batches", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--slots", type=int, default=3)
+    ap.add_argument("--only", choices=["recv", "send", "both"], default=None,
+                    help="time one mode only (for tracing)")
     args = ap.parse_args()
 
     import torch
@@ -139,9 +146,13 @@ def main():
         assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], dev_events[r.eventNum, :B])
 
     res = {"config": f"host path: {BE} x {B} B events per batch, MTU {args.mtu}, pinned buffers, "
-                     f"2 streams per direction (H2D+kernel, D2H), {S} rotating buffer sets",
-           "recv_GiBps": round(run("recv"), 2), "send_GiBps": round(run("send"), 2),
-           "both_GiBps_each_direction": round(run("both"), 2)}
+                     f"2 streams per direction (H2D+kernel, D2H), {S} rotating buffer sets"}
+    if args.only:
+        res[args.only + "_GiBps"] = round(run(args.only), 2)
+        print(json.dumps(res), flush=True)
+        return
+    res.update({"recv_GiBps": round(run("recv"), 2), "send_GiBps": round(run("send"), 2),
+                "both_GiBps_each_direction": round(run("both"), 2)})
     # PCIe alone: the same copies without kernels
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -106,11 +106,20 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # E2SAR_BENCH_BACKEND=gloo + E2SAR_BENCH_SHARE_GPU=1 rehearse the N>1 flow with every
+    # rank on GPU 0 (a one-GPU box); the driver's multi-GPU runs use RCCL ("nccl").
+    backend = os.environ.get("E2SAR_BENCH_BACKEND", "nccl")
+    if os.environ.get("E2SAR_BENCH_SHARE_GPU") == "1":
+        local = 0
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ctx = sar.Context(local)
+    coll_dev = dev if backend == "nccl" else torch.device("cpu")
 
     B = args.event_bytes
     E = args.events
@@ -254,9 +263,10 @@ def main():
         ids = torch.tensor([evnum(i) for i in range(E)], dtype=torch.int64, device=dev)
         table = torch.stack([ids, sums], dim=1)
         if world > 1:
+            table = table.to(coll_dev)
             allt = [torch.empty_like(table) for _ in range(world)]
             dist.all_gather(allt, table)
-            table = torch.cat(allt)
+            table = torch.cat(allt).to(dev)
         ref = {int(a): int(b) for a, b in table.tolist()}
         owned = [e for e in ref if e % world == rank]
         ok = (len(recs) == len(owned) and st.inProgress == 0 and st.badHeaderDiscards == 0)
@@ -327,7 +337,7 @@ def main():
         dist.barrier()
     elapsed = t1 - t0
     if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 

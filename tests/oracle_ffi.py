@@ -56,6 +56,11 @@ def lib() -> C.CDLL:
         L.e2o_reas_push.argtypes = [vp, u8p, sz]
         L.e2o_reas_push_batch.restype = None
         L.e2o_reas_push_batch.argtypes = [vp, u8p, sz, sz, u8p]
+        L.e2o_reas_pop.restype = C.c_int
+        L.e2o_reas_pop.argtypes = [vp, C.POINTER(C.POINTER(C.c_uint8)), C.POINTER(sz), C.POINTER(C.c_uint64),
+                                   C.POINTER(C.c_uint16)]
+        L.e2o_free.restype = None
+        L.e2o_free.argtypes = [vp]
         L.e2o_reas_pop_into.restype = C.c_longlong
         L.e2o_reas_pop_into.argtypes = [vp, u8p, sz, C.POINTER(C.c_uint64), C.POINTER(C.c_uint16)]
         L.e2o_reas_gc.restype = sz

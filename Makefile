@@ -44,3 +44,11 @@ e2sar_amd/e2sar_py$(PYEXT): e2sar_amd/csrc/host/py_e2sar.cpp $(HOST_HDRS) includ
 		-L$(LIBDIR) -le2sar_amd -le2sar_hip -Wl,-rpath,'$$ORIGIN/lib'
 
 all: e2sar_amd/e2sar_py$(PYEXT)
+
+# ---- e2sar_perf-shaped tool over the C++ facade ----
+build/e2sar_perf: tools/e2sar_perf.cpp $(HOST_HDRS) include/e2sar_amd/e2sarHeaders.hpp $(LIBDIR)/libe2sar_amd.so
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -Iinclude -o $@ tools/e2sar_perf.cpp -L$(LIBDIR) -le2sar_amd -le2sar_hip \
+		-Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+all: build/e2sar_perf

@@ -84,6 +84,7 @@ struct Segmenter::Impl {
     std::atomic<bool> stop{false};
     bool started = false;
     std::mt19937 rng{std::random_device{}()};
+    std::chrono::steady_clock::time_point paceNext{};   // rate pacing: earliest start of the next event
 
     Impl(const EjfatURI &u, uint16_t did, uint32_t esid, std::vector<int> c, const SegmenterFlags &f)
         : uri(u), dataId(did), eventSrcId(esid), flags(f), cores(std::move(c))
@@ -260,6 +261,20 @@ result<int> Segmenter::Impl::sendBatch(std::vector<Item> &items)
                 mv[k].msg_hdr.msg_namelen = dstLen;
             }
         }
+        // start-to-start pacing, as the reference's busy wait from the dispatch time
+        // (cpp:401, 447-450): the next event may start interval after this one started
+        if (flags.rateGbps > 0) {
+            const auto now = std::chrono::steady_clock::now();
+            if (paceNext > now) {
+                if (paceNext - now > std::chrono::microseconds(200))
+                    std::this_thread::sleep_until(paceNext - std::chrono::microseconds(100));
+                while (std::chrono::steady_clock::now() < paceNext) {
+                }
+            } else {
+                paceNext = now;   // behind schedule: no credit is banked
+            }
+            paceNext += std::chrono::nanoseconds((int64_t)((double)items[i].bytes * 8.0 / flags.rateGbps));
+        }
         uint32_t sent = 0;
         while (sent < n) {
             const int r = sendmmsg(fds[s], mv.data() + sent, n - sent, 0);
@@ -277,10 +292,6 @@ result<int> Segmenter::Impl::sendBatch(std::vector<Item> &items)
             sent += (uint32_t)r;
         }
         msgCnt += n;
-        if (flags.rateGbps > 0) {   // inter-event pacing, cpp:401,447-450
-            const double us = (double)items[i].bytes * 8.0 / (flags.rateGbps * 1000.0);
-            std::this_thread::sleep_for(std::chrono::microseconds((int64_t)us));
-        }
     }
     return 0;
 }

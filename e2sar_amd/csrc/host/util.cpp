@@ -1,7 +1,10 @@
 // util.cpp -- EjfatURI (data-path subset), get_PortRange, INI flag loading.
 #include <algorithm>
 #include <cctype>
+#include <cerrno>
 #include <cstdlib>
+#include <cstring>
+#include <unistd.h>
 #include <fstream>
 #include <map>
 #include <sstream>
@@ -12,7 +15,7 @@
 namespace e2sar {
 
 // "ejfat[s]://[token@]host:port/lb/<id>?sync=ip:port&data=ip[:port]&data=[v6][:port]"
-EjfatURI::EjfatURI(const std::string &uri)
+EjfatURI::EjfatURI(const std::string &uri, TokenType, bool)
 {
     const auto sch = uri.find("://");
     if (sch == std::string::npos) throw E2SARException("Unable to parse URI: " + uri);
@@ -199,5 +202,37 @@ result<ReassemblerFlagsT> ReassemblerFlagsT::getFromINI(const std::string &iniFi
     f.arenaBytes = (size_t)detail::ini_num(m, "device.arenaBytes", (double)f.arenaBytes);
     return f;
 }
+
+}  // namespace e2sar
+
+namespace e2sar {
+
+result<EjfatURI> EjfatURI::getFromString(const std::string &uri, TokenType tt, bool preferV6) noexcept
+{
+    try {
+        return EjfatURI(uri, tt, preferV6);
+    } catch (const std::exception &e) {
+        return E2SARErrorInfo{E2SARErrorc::ParseError, e.what()};
+    }
+}
+
+result<EjfatURI> EjfatURI::getFromEnv(const std::string &envVar, TokenType tt, bool preferV6) noexcept
+{
+    const char *v = std::getenv(envVar.c_str());
+    if (!v) return E2SARErrorInfo{E2SARErrorc::Undefined, "environment variable " + envVar + " not defined"};
+    return getFromString(v, tt, preferV6);
+}
+
+const std::string get_Version() { return "0.3.2-mi355x"; }
+
+namespace NetUtil {
+result<std::string> getHostName() noexcept
+{
+    char buf[256];
+    if (gethostname(buf, sizeof(buf)) != 0) return E2SARErrorInfo{E2SARErrorc::SystemError, strerror(errno)};
+    buf[sizeof(buf) - 1] = 0;
+    return std::string(buf);
+}
+}  // namespace NetUtil
 
 }  // namespace e2sar

@@ -96,7 +96,15 @@ public:
 // The data-path part of EjfatURI: "ejfat[s]://[token@]host:port/lb/<id>?sync=ip:port&data=ip[:port]"
 class EjfatURI {
 public:
-    explicit EjfatURI(const std::string &uri);
+    // e2sarUtil.hpp: token kinds; only the data-path fields of the URI are used here
+    enum class TokenType { admin = 0, instance = 1, session = 2 };
+
+    explicit EjfatURI(const std::string &uri, TokenType tt = TokenType::admin, bool preferV6 = false);
+    // e2sarUtil.hpp getFromString / getFromEnv: parse errors become E2SARErrorc::ParseError
+    static result<EjfatURI> getFromString(const std::string &uri, TokenType tt = TokenType::admin,
+                                          bool preferV6 = false) noexcept;
+    static result<EjfatURI> getFromEnv(const std::string &envVar = "EJFAT_URI", TokenType tt = TokenType::admin,
+                                       bool preferV6 = false) noexcept;
     bool has_dataAddrv4() const { return !dataV4.empty(); }
     bool has_dataAddrv6() const { return !dataV6.empty(); }
     bool has_dataAddr() const { return has_dataAddrv4() || has_dataAddrv6(); }
@@ -113,6 +121,14 @@ private:
 
 // get_PortRange (e2sarCP.hpp:772-798)
 int get_PortRange(int source_count) noexcept;
+
+// e2sar.hpp get_Version
+const std::string get_Version();
+
+// e2sarNetUtil.hpp: the one helper the data-path tools use
+namespace NetUtil {
+result<std::string> getHostName() noexcept;
+}
 
 // Flag structs are declared at namespace scope so their default member initialisers
 // can serve as default arguments; Segmenter::SegmenterFlags and

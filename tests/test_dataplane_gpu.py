@@ -6,6 +6,7 @@ expecting the LB header the missing load balancer would have stripped.  Datagram
 captured on a plain socket are compared bit-for-bit with the oracle, taking the
 per-event LB tick and entropy (random by design in the reference) from the datagram.
 """
+import os
 import socket
 import threading
 import time
@@ -337,3 +338,18 @@ def test_b2b_large_events_jumbo(E):
         assert np.array_equal(got[k], e)
     assert reas.getStats().eventSuccess == 24
     reas.stopThreads()
+
+
+@pytest.mark.gpu
+def test_e2sar_perf_tool_loopback():
+    # the e2sar_perf-shaped tool (tools/e2sar_perf.cpp) end to end over UDP loopback:
+    # Segmenter -> seg_kernel -> sendmmsg -> recvmmsg -> reas_kernel -> recvEvent
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "e2sar_perf")
+    if not os.path.exists(exe):
+        pytest.fail("build/e2sar_perf missing: run make")
+    r = subprocess.run([exe, "--loopback", "-l", "100000", "-n", "50", "-m", "9000", "--rate", "2",
+                        "--port", "10400"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "50 of 50 events intact" in r.stdout
+    assert "eventSuccess=50" in r.stdout and "badHeaderDiscards=0" in r.stdout

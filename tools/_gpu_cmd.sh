@@ -1,4 +1,7 @@
-mkdir -p gpurun_out/n2
-export E2SAR_BENCH_BACKEND=gloo E2SAR_BENCH_SHARE_GPU=1
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --cpu-seconds 0 --events 256 > gpurun_out/n2/own.json 2> gpurun_out/n2/own.err || { tail -20 gpurun_out/n2/own.err; exit 1; }
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29518 bench.py --gpus 4 --steps 10 --warmup 2 --cpu-seconds 0 --events 128 > gpurun_out/n2/own4.json 2> gpurun_out/n2/own4.err || { tail -20 gpurun_out/n2/own4.err; exit 1; }
+mkdir -p gpurun_out/perf2
+timeout -k 10 300 python -m pytest tests/test_dataplane_gpu.py -x -q > gpurun_out/perf2/tests.log 2>&1 || { tail -30 gpurun_out/perf2/tests.log; exit 1; }
+tail -1 gpurun_out/perf2/tests.log
+for r in 5 10 20; do
+timeout -k 10 120 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m 9000 --rate $r > gpurun_out/perf2/lo_9000_r$r.log 2>&1; echo "rc=$?" >> gpurun_out/perf2/lo_9000_r$r.log
+done
+timeout -k 10 120 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m 1500 --rate 5 > gpurun_out/perf2/lo_1500_r5.log 2>&1; echo "rc=$?" >> gpurun_out/perf2/lo_1500_r5.log

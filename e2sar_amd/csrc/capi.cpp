@@ -57,6 +57,16 @@ struct e2sar_hip_reas {
     std::mutex mu;
 };
 
+// Free whatever a partly built reassembler holds (every pointer starts null).
+static void reas_release(e2sar_hip_reas *r)
+{
+    if (r->altSlots) (void)hipFree(r->altSlots);
+    if (r->alt.arena && r->alt.arena != r->dev.arena) (void)hipFree(r->alt.arena);
+    if (r->dev.arena) (void)hipFree(r->dev.arena);
+    if (r->stateMem) (void)hipFree(r->stateMem);
+    delete r;
+}
+
 extern "C" {
 
 int e2sar_hip_abi_version(void) { return E2SAR_HIP_ABI_VERSION; }
@@ -275,14 +285,21 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     const size_t total = slotsB + ctlB + compB + lostB;
     hipError_t e = hipMalloc(&r->stateMem, total);
     if (e != hipSuccess) {
-        delete r;
+        r->stateMem = nullptr;
+        reas_release(r);
         return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(state): ") + hipGetErrorString(e));
     }
     e = hipMalloc(reinterpret_cast<void **>(&r->dev.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
     if (e != hipSuccess) {
-        (void)hipFree(r->stateMem);
-        delete r;
+        r->dev.arena = nullptr;
+        reas_release(r);
         return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(arena): ") + hipGetErrorString(e));
+    }
+    // reas_stream_kernel takes a payload's 16-byte phase in its event buffer from the
+    // datagram's bufferOffset alone: event buffers are 256-byte aligned in a 256-byte-aligned arena
+    if ((reinterpret_cast<uintptr_t>(r->dev.arena) & 255u) != 0) {
+        reas_release(r);
+        return fail(E2SAR_HIP_ERR_MEMORY, "arena not 256-byte aligned");
     }
     auto *base = static_cast<uint8_t *>(r->stateMem);
     r->dev.slots = reinterpret_cast<ReasSlot *>(base);
@@ -296,20 +313,18 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->dev.lostCapacity = cfg->lostCapacity;
     r->dev.withLB = cfg->withLBHeader ? 1 : 0;
     r->alt = r->dev;
+    r->alt.arena = nullptr;
     if (cfg->flags & E2SAR_HIP_REAS_COMPACTABLE) {
         e = hipMalloc(&r->altSlots, slotsB);
         if (e == hipSuccess) e = hipMalloc(reinterpret_cast<void **>(&r->alt.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
         if (e != hipSuccess) {
-            (void)hipFree(r->altSlots);
-            (void)hipFree(r->stateMem);
-            (void)hipFree(r->dev.arena);
-            delete r;
+            reas_release(r);
             return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(alternate arena): ") + hipGetErrorString(e));
         }
         r->alt.slots = reinterpret_cast<ReasSlot *>(r->altSlots);
         e = hipMemsetAsync(r->altSlots, 0, slotsB, ctx->stream);
         if (e != hipSuccess) {
-            delete r;
+            reas_release(r);
             return hip_fail(e, "alternate table init");
         }
     } else {
@@ -319,9 +334,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     e = hipMemsetAsync(r->stateMem, 0, total, ctx->stream);
     if (e == hipSuccess) e = hipStreamSynchronize(ctx->stream);
     if (e != hipSuccess) {
-        (void)hipFree(r->stateMem);
-        (void)hipFree(r->dev.arena);
-        delete r;
+        reas_release(r);
         return hip_fail(e, "state init");
     }
     *out = r;

@@ -23,9 +23,6 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
-#ifndef E2SAR_REAS_EXPERIMENT_NOCLASSIFY
-#define E2SAR_REAS_EXPERIMENT_NOCLASSIFY 0
-#endif
 // Occupancy cap of the fused reassembly kernel (0 = whatever its registers allow).
 #ifndef E2SAR_REAS_WAVES
 #define E2SAR_REAS_WAVES 0
@@ -41,6 +38,28 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
 #define E2SAR_REAS_CHUNKS_PER_BLOCK 9216u
 #endif
+
+// Timeline trace (experiment builds only, -DE2SAR_TRACE=1): per workgroup, s_memrealtime
+// (100 MHz) at start, after classification, after the barrier and at the end, plus HW_ID.
+#ifndef E2SAR_TRACE
+#define E2SAR_TRACE 0
+#endif
+#if E2SAR_TRACE
+__device__ uint64_t g_trace[2][8192 * 4];
+#define TRACE_AT(k, slot, i) \
+    do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
+#else
+#define TRACE_AT(k, slot, i) do {} while (0)
+#endif
+__device__ __forceinline__ uint64_t trace_now() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ uint64_t trace_hwid()
+{
+    uint32_t v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+    uint32_t x;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(x));
+    return ((uint64_t)x << 32) | v;
+}
 
 // Global-address-space accessors: the event/packet/arena pointers reach the kernels
 // through descriptor tables, so without these hipcc falls back to flat_* accesses.
@@ -58,12 +77,35 @@ __device__ __forceinline__ u32x4 ld16_nt(const uint8_t *p)
     return __builtin_nontemporal_load((const E2SAR_GLOBAL u32x4_a4 *)(p));
 }
 __device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4 *)(p)); }
-// 16-byte non-temporal store at a dword-aligned (not 16-byte-aligned) address
+// 16-byte store at a dword-aligned (not 16-byte-aligned) address (non-temporal unless
+// E2SAR_REAS_NT_STORE=0)
+#ifndef E2SAR_REAS_NT_STORE
+#define E2SAR_REAS_NT_STORE 1
+#endif
 __device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v)
 {
+#if E2SAR_REAS_NT_STORE
     __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4_a4 *)(p));
+#else
+    *(E2SAR_GLOBAL u32x4_a4 *)(p) = v;
+#endif
 }
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
+
+// Workgroup barrier that orders LDS only.  __syncthreads() also waits for every global
+// load and atomic the wave has outstanding; here a classifier's fire-and-forget counter
+// atomics and the payload loads of the other waves stay in flight across it.
+#ifndef E2SAR_REAS_LDS_BARRIER
+#define E2SAR_REAS_LDS_BARRIER 1
+#endif
+__device__ __forceinline__ void lds_barrier()
+{
+#if E2SAR_REAS_LDS_BARRIER
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+#else
+    __syncthreads();
+#endif
+}
 
 // ---------------------------------------------------------------------------------
 // segmentation
@@ -169,6 +211,7 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
                                                      uint32_t maxPld, uint8_t *__restrict__ pkts,
                                                      uint32_t stride, uint32_t *__restrict__ lens)
 {
+    TRACE_AT(1, 0, trace_now());
     const uint32_t e = blockIdx.x / blocksPerEvent;
     const uint32_t bx = blockIdx.x - e * blocksPerEvent;
     const e2sar_hip_seg_event ev = events[e];
@@ -259,16 +302,25 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
         }
         st16(out + 16u * jj[u], o);
     }
+#if E2SAR_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    TRACE_AT(1, 2, trace_hwid());
+    TRACE_AT(1, 3, trace_now());
+#endif
 }
 
 // ---------------------------------------------------------------------------------
 // reassembly: event table protocol
 //
-// slot.state: EMPTY -> BUSY (CAS by the inserting lane) -> READY (after the key,
-// length and buffer offset are stored) -> DONE (completed) / LOST (GC'd).  Every
-// cross-lane hand-off of slot fields uses agent-scope atomic loads/stores (sc1) with
-// the publishing lane's own s_waitcnt vmcnt(0) before the READY store
-// (MI355X_MICROARCH.md 'Valid forms', R1 row: one storing lane, sc1 payload + flag).
+// slot.state: EMPTY -> BUSY (CAS by the inserting lane) -> READY (published with the key)
+// -> DONE (completed) / LOST (GC'd).  A lookup claims first: CAS EMPTY->BUSY either makes
+// the lane the creator (one round trip) or returns the slot's state.  The creator takes its
+// buffer from the arena and publishes record B {bufOff, bytes, bvalid=1} and record A
+// {READY, dataId, eventNum} as two 16-byte agent-scope (sc1) stores, without waiting for
+// them; other lanes read A and B together (two sc1 loads, one round trip) until A is READY
+// and B valid.  acc starts at 0 because a slot is EMPTY only after it was zeroed (slots
+// are never reused within an arena epoch).
 
 enum : uint32_t { kEmpty = 0, kBusy = 1, kReady = 2, kDone = 3, kLost = 4 };
 
@@ -283,6 +335,22 @@ template <typename T>
 __device__ __forceinline__ void st_agent(T *p, typename id_t_<T>::type v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 16-byte agent-scope store and the pair of 16-byte agent-scope loads of records A and B
+// (the forms the compiler emits for 4/8-byte agent-scope atomics, at 16 bytes).  The
+// loads wait for their own results inside the asm.
+__device__ __forceinline__ void st16_agent(void *p, u32x4 v)
+{
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void ld_slot_ab(const ReasSlot *sl, u32x4 &A, u32x4 &B)
+{
+    asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
+                 "global_load_dwordx4 %1, %2, off offset:16 sc1\n\t"
+                 "s_waitcnt vmcnt(0)"
+                 : "=&v"(A), "=&v"(B)
+                 : "v"(sl)
+                 : "memory");
 }
 
 __device__ __forceinline__ uint32_t slot_hash(uint64_t ev, uint32_t d, uint32_t mask)
@@ -306,66 +374,74 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint64_t kNoBuf = ~0ull;
 constexpr uint32_t kSpinLimit = 1u << 22;
 
-__device__ LookupResult find_or_create(const ReasDev &R, uint64_t ev, uint32_t d,
-                                       uint32_t blen, uint64_t now)
+// Called by a whole wave: lanes with want == false only take part in the loop.  The wave
+// loops until every wanting lane has a result, and every pass is straight-line (claim;
+// creators publish; the others read), so a lane never waits inside a divergent branch
+// for a slot that another lane of the same wave is still creating.
+__device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
+                                       uint64_t now)
 {
     LookupResult res{kNoSlot, 0, kNoBuf};
     const uint32_t mask = R.tableSlots - 1u;
     uint32_t h = slot_hash(ev, d, mask);
-    for (uint32_t probe = 0; probe < R.tableSlots; probe++, h = (h + 1u) & mask) {
-        ReasSlot *sl = R.slots + h;
-        uint32_t stt = ld_agent(&sl->state);
-        if (stt == kEmpty) {
+    uint32_t probes = 0, spins = 0;
+    bool active = want;
+    while (__ballot(active)) {
+        bool waiting = false, advance = false;
+        if (active) {
+            ReasSlot *sl = R.slots + h;
             const uint32_t old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
             if (old == kEmpty) {
-                // this lane owns the slot: publish key, length, buffer, then READY
+                // this lane owns the slot: buffer, then records B and A
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
                 uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
                 if (boff + blen > R.arenaBytes) {
                     boff = kNoBuf;
                     atomicOr(&R.ctl->errorFlags, 2u);
                 }
-                st_agent(&sl->eventNum, ev);
-                st_agent(&sl->dataId, d);
-                st_agent(&sl->bytes, blen);
-                st_agent(&sl->bufOff, boff);
                 st_agent(&sl->created, now);
-                st_agent(&sl->acc, 0ull);
+                st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, 1u});
+                st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
                 atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), 1ull);
                 atomicAdd(&R.ctl->tableUsed, 1u);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                st_agent(&sl->state, (uint32_t)kReady);
                 res.slot = h;
                 res.bytes = blen;
                 res.bufOff = boff;
-                return res;
+                active = false;
+            } else if (old == kBusy || old == kReady) {
+                u32x4 A, B;
+                ld_slot_ab(sl, A, B);
+                if (A.x == kReady && B.w != 0u) {
+                    if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
+                        res.slot = h;
+                        res.bytes = B.z;
+                        res.bufOff = ((uint64_t)B.y << 32) | B.x;
+                        active = false;
+                    } else {
+                        advance = true;                                // another event's slot
+                    }
+                } else if (A.x == kBusy || A.x == kReady) {
+                    waiting = true;                                    // not published yet
+                } else {
+                    advance = true;                                    // DONE / LOST meanwhile
+                }
+            } else {
+                advance = true;                                        // DONE / LOST
             }
-            stt = old;
-        }
-        uint32_t spins = 0;
-        while (stt == kBusy) {
-            __builtin_amdgcn_s_sleep(1);
-            stt = ld_agent(&sl->state);
-            if (++spins > kSpinLimit) {
+            if (advance) {
+                h = (h + 1u) & mask;
+                if (++probes >= R.tableSlots) {
+                    atomicOr(&R.ctl->errorFlags, 1u);
+                    active = false;
+                }
+            }
+            if (waiting && ++spins > kSpinLimit) {
                 atomicOr(&R.ctl->errorFlags, 4u);
-                return res;
+                active = false;
             }
         }
-        if (stt == kReady) {
-            // one round trip for the whole key + buffer record (all stored before READY)
-            const uint64_t sev = ld_agent(&sl->eventNum);
-            const uint32_t sd = ld_agent(&sl->dataId);
-            const uint32_t sb = ld_agent(&sl->bytes);
-            const uint64_t so = ld_agent(&sl->bufOff);
-            if (sev == ev && sd == d) {
-                res.slot = h;
-                res.bytes = sb;
-                res.bufOff = so;
-                return res;
-            }
-        }
+        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(1);
     }
-    atomicOr(&R.ctl->errorFlags, 1u);
     return res;
 }
 
@@ -462,8 +538,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     const bool head = ok && (lane == 0 || !pok || pev != ev || pd != d);
     const bool tail = ok && (lane == 63 || !nok || nev != ev || nd != d);
 
-    LookupResult lr{kNoSlot, 0, kNoBuf};
-    if (head) lr = find_or_create(R, ev, d, blen, now);
+    const LookupResult lr = find_or_create(R, head, ev, d, blen, now);
 
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
@@ -629,28 +704,78 @@ __device__ __forceinline__ PktInfo ld_info(const PktInfo *p)
     return r;
 }
 
-// reas_kernel: one block = G consecutive datagrams, G*spc <= 256*U 16-byte chunks, so
-// each thread owns at most U chunks of SOURCE-aligned datagram bytes.
-//   1. wave 0 issues the header loads of the G datagrams;
-//   2. every thread issues its U 16-byte payload loads (aligned, inside the datagram
-//      slots -- no classification needed to know where to read);
-//   3. wave 0 classifies (event table lookup/insert, run sums, counter atomics) while
-//      those loads are in flight, and leaves each datagram's destination in LDS;
-//   4. every thread stores its chunks to event + bufferOffset + (16c - header): whole
-//      16-byte stores inside the payload, whole dwords at the two edges, bytes only for
-//      a sub-dword event tail or a datagram whose offset is not dword-congruent;
+// Destination-aligned form of the same copy: chunk c of a payload whose phase in its event
+// buffer is a (= bufferOffset mod 16; event buffers are 256-byte aligned in a 256-byte
+// aligned arena) covers event bytes [(dst & ~15) + 16c, +16), i.e. datagram bytes from
+// r = hl + 16c - a -- a multiple of 4 for a dword-congruent payload, so one dword-aligned
+// 16-byte load, slid back by sh inside the slot at its end and shifted down in registers,
+// feeds one aligned 16-byte store.
+__device__ __forceinline__ uint32_t da_window(uint32_t c, uint32_t a, uint32_t hl, uint32_t stride, uint32_t &sh)
+{
+    const uint32_t r = hl + 16u * c - a;
+    sh = (r + 16u > stride) ? r + 16u - stride : 0u;
+    return r - sh;
+}
+
+// Store destination-aligned chunk c (loaded from the window of da_window) of the datagram
+// at dgram: whole aligned 16-byte stores inside the payload, dwords at its two edges,
+// bytes for a sub-dword event tail, byte copies for a payload that is not dword-congruent.
+__device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, const uint8_t *dgram, uint32_t stride)
+{
+    const uint32_t a = (uint32_t)pi.dst & 15u;
+    if (pi.plen == 0u || 16u * c >= a + pi.plen) return;          // dropped, or past the payload
+    uint8_t *D = reinterpret_cast<uint8_t *>((pi.dst & ~15ull) + 16ull * c);
+    const uint32_t lo = (c == 0u) ? a : 0u;
+    const uint32_t hi = (a + pi.plen - 16u * c < 16u) ? a + pi.plen - 16u * c : 16u;
+    if ((a & 3u) == 0u) {
+        uint32_t sh;
+        (void)da_window(c, a, pi.hl, stride, sh);
+        const u32x4 o = rot_down(x, sh >> 2);
+        if (lo == 0u && hi == 16u) {
+            st16_nt(D, o);
+        } else {
+#pragma unroll
+            for (uint32_t d = 0; d < 4; d++)
+                if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
+            const uint32_t t = hi & ~3u;                               // sub-dword event tail
+            if (t < hi && t >= lo) store_bytes(D, o, t, hi);
+        }
+    } else {
+        const uint8_t *s = dgram + pi.hl + 16u * c - a;                // + lo >= hl
+        for (uint32_t b = lo; b < hi; b++) st1(D + b, ld1(s + b));
+    }
+}
+
+// Per-workgroup LDS of the fused reassembly: destinations of the group's datagrams, and
+// the run tails' completion state (only the atomic's return value stays in registers during
+// the copy, which keeps the kernel's occupancy up).
+struct ReasGroupLds {
+    PktInfo info[64];
+    uint64_t ev[64], boff[64];
+    uint32_t slot[64], bytes[64], d[64], rb[64], rc[64], tail[64];
+};
+
+// One group of gn <= 64 consecutive datagrams [g*G, g*G + gn), by the whole workgroup:
+//   1. every wave loads the group's headers (lane p: datagram p); the load geometry of each
+//      payload -- its phase in the event buffer and its length -- comes from them;
+//   2. every thread issues its first U destination-aligned 16-byte payload loads;
+//   3. wave 0 classifies (event table lookup/insert, run sums, counter atomics) while those
+//      loads are in flight, and leaves each datagram's destination in LDS;
+//   4. every thread stores its chunks (da_store), then loads and stores the rest round by
+//      round (U chunks of 16 bytes per thread per round);
 //   5. the run tails complete events (their atomic results are consumed last).
 template <int U>
-__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
-                                                      uint32_t stride, const uint32_t *__restrict__ lens,
-                                                      uint32_t n, uint64_t now, uint32_t G)
+__device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                           const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
+                                           uint32_t g, ReasGroupLds &L)
 {
-    __shared__ PktInfo sinfo[64];
-    const uint32_t g0 = blockIdx.x * G;
+    const uint32_t tx = threadIdx.x;
+    const uint32_t g0 = g * G;
     const uint32_t gn = (n - g0 < G) ? n - g0 : G;
-    const bool w0 = threadIdx.x < 64;
-    const uint32_t lane = threadIdx.x & 63u;
+    const bool w0 = tx < 64;
+    const uint32_t lane = tx & 63u;
 
+    TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
 
@@ -658,7 +783,6 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(Reas
     const uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
-    u32x4 x[U];
     // chunk i -> (datagram, chunk within it); recomputed at store time rather than kept
     // live across the classification (register pressure sets this kernel's occupancy)
     auto split_chunk = [&](uint32_t i, uint32_t &p, uint32_t &c) {
@@ -668,79 +792,91 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(Reas
         else if ((p + 1u) * spc <= ic) p++;
         c = ic - p * spc;
     };
-    auto issue = [&](uint32_t r0) {
+    const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
+    const uint32_t gPhase = bswap32(raw.re.y) & 15u;
+    const uint32_t gPlen = (raw.len >= hl) ? ((raw.len < stride) ? raw.len : stride) - hl : 0u;
+    auto issue = [&](uint32_t r0, u32x4(&xs)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + tx;
             uint32_t p, c;
-            split_chunk(r0 + (uint32_t)u * kBlock + threadIdx.x, p, c);
-            x[u] = ld16(bpk + (uint64_t)p * stride + 16u * c);
+            split_chunk(i, p, c);
+            const uint32_t a = __shfl(gPhase, (int)p), plen = __shfl(gPlen, (int)p);
+            uint32_t off = 0, sh;
+            if (i < nch && 16u * c < a + plen && (a & 3u) == 0u) off = p * stride + da_window(c, a, hl, stride, sh);
+            xs[u] = ld16(bpk + off);
         }
     };
-    issue(0);                          // round 0 is in flight while wave 0 classifies
-
-    // wave 0's run-tail state waits in LDS during the copy (only the atomic's return value
-    // stays in registers), which keeps the kernel at 8 waves per SIMD
-    __shared__ uint64_t sEv[64], sBoff[64];
-    __shared__ uint32_t sSlot[64], sBytes[64], sD[64], sRb[64], sRc[64], sTail[64];
-    unsigned long long old = 0;
-#if E2SAR_REAS_EXPERIMENT_NOCLASSIFY
-    // A/B experiment only (never shipped): destination straight from the header with no
-    // table, no atomics -- the pure-copy floor of this kernel's access pattern.
-    if (w0) {
-        const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
-        const uint32_t blen = bswap32(raw.re.z), off = bswap32(raw.re.y);
-        const uint64_t ev = ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4);
-        const uint64_t es = ((uint64_t)blen + 255ull) & ~255ull;
-        PktInfo pi;
-        pi.dst = (uint64_t)(R.arena + (ev & 127ull) * es + off);
-        pi.plen = lane < gn ? raw.len - hl : 0u;
-        pi.hl = hl;
-        sinfo[lane] = pi;
-    }
-#else
-    if (w0) {
-        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, blockIdx.x);
-        sinfo[lane] = cl.info;
-        old = cl.old;
-        sEv[lane] = cl.ev;
-        sBoff[lane] = cl.boff;
-        sSlot[lane] = cl.slot;
-        sBytes[lane] = cl.sbytes;
-        sD[lane] = cl.d;
-        sRb[lane] = cl.rb;
-        sRc[lane] = cl.rc;
-        sTail[lane] = cl.tailAdd ? 1u : 0u;
-    }
-#endif
-    __syncthreads();
-
-    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
-        if (r0) issue(r0);
+    auto store = [&](uint32_t r0, const u32x4(&xs)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            const uint32_t i = r0 + (uint32_t)u * kBlock + tx;
             if (i >= nch) continue;
             uint32_t p, c;
             split_chunk(i, p, c);
-            scatter_chunk(sinfo[p], c, x[u]);
+            da_store(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
         }
+    };
+    u32x4 x[U];
+    issue(0u, x);                      // round 0 is in flight while wave 0 classifies
+
+    unsigned long long old = 0;
+    if (w0) {
+        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g);
+        L.info[lane] = cl.info;
+        old = cl.old;
+        L.ev[lane] = cl.ev;
+        L.boff[lane] = cl.boff;
+        L.slot[lane] = cl.slot;
+        L.bytes[lane] = cl.sbytes;
+        L.d[lane] = cl.d;
+        L.rb[lane] = cl.rb;
+        L.rc[lane] = cl.rc;
+        L.tail[lane] = cl.tailAdd ? 1u : 0u;
+        TRACE_AT(0, 1, trace_now());
+    }
+    lds_barrier();
+    TRACE_AT(0, 2, trace_hwid());
+
+    store(0u, x);
+    for (uint32_t r0 = (uint32_t)(kBlock * U); r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+        issue(r0, x);
+        store(r0, x);
     }
 
-#if !E2SAR_REAS_EXPERIMENT_NOCLASSIFY
-    if (w0 && sTail[lane]) {
+    if (w0 && L.tail[lane]) {
         Classified cl;
         cl.old = old;
-        cl.ev = sEv[lane];
-        cl.boff = sBoff[lane];
-        cl.slot = sSlot[lane];
-        cl.sbytes = sBytes[lane];
-        cl.d = sD[lane];
-        cl.rb = sRb[lane];
-        cl.rc = sRc[lane];
+        cl.ev = L.ev[lane];
+        cl.boff = L.boff[lane];
+        cl.slot = L.slot[lane];
+        cl.sbytes = L.bytes[lane];
+        cl.d = L.d[lane];
+        cl.rb = L.rb[lane];
+        cl.rc = L.rc[lane];
         cl.tailAdd = true;
         classify_finish(R, cl);
     }
+#if E2SAR_TRACE
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    TRACE_AT(0, 3, trace_now());
 #endif
+}
+
+// reas_kernel: workgroup b reassembles datagrams [b*G, b*G + G) of the batch.
+// (A/B: a resident grid drawing groups dynamically from per-XCD work counters, to even
+// out XCDs that stream at different rates, ran 1.7-2.2x slower: a workgroup's groups are
+// then classified one after another and every classification -- ~7 us of dependent table
+// round trips -- sits in front of its copy, where the one-shot grid classifies all groups
+// at once while the first round of loads is in flight.)
+template <int U>
+__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+                                                                           uint32_t stride, const uint32_t *__restrict__ lens,
+                                                                           uint32_t n, uint64_t now, uint32_t G)
+{
+    __shared__ ReasGroupLds L;
+    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L);
 }
 
 // ---------------------------------------------------------------------------------
@@ -968,6 +1104,7 @@ __global__ __launch_bounds__(kBlock) void reas_compact_kernel(ReasDev from, Reas
                 d->eventNum = sl->eventNum;
                 d->acc = sl->acc;
                 d->bufOff = off;
+                d->bvalid = 1u;
                 d->created = sl->created;
                 d->state = kReady;
                 atomicAdd(&to.ctl->compactUsed, 1u);
@@ -1048,17 +1185,27 @@ static uint32_t scatter_group_size(uint32_t stride)
     return G;
 }
 
+static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
+{
+    const char *v = getenv(var);
+    if (!v) return dflt;
+    const long x = atol(v);
+    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
+}
+
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
-    // (A/B: at MTU 1500 2K-chunk blocks lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
-    // 8 MiB events 4K chunks (4 datagrams per block) lose 27 % to 9K-18K: per-event counter
-    // and table traffic grows with blocks per event)
-    const uint32_t G = scatter_group_size(stride);
-    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_REAS_LDS"), stream, R, pkts, stride, lens, n,
-                       now, G);
+    // datagrams per workgroup: at most E2SAR_REAS_CHUNKS 16-byte chunks (A/B knob), <= 64.
+    // (A/B: at MTU 1500 2K-chunk groups lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
+    // 8 MiB events 4K chunks (4 datagrams per group) lose 27 % to 9K-18K: per-event counter
+    // and table traffic grows with groups per event)
+    const uint32_t spc = stride >> 4, budget = env_u32("E2SAR_REAS_CHUNKS", E2SAR_REAS_CHUNKS_PER_BLOCK, 64, 1u << 20);
+    uint32_t G = 64;
+    while (G > 1 && G * spc > budget) G >>= 1;
+    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G);
     return hipGetLastError();
 }
 
@@ -1296,3 +1443,19 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
 }
 
 }  // namespace e2sar_amd
+
+#if E2SAR_TRACE
+// Experiment builds only: copy the timeline of the last reas_kernel (k = 0) or seg_kernel
+// (k = 1) launch, 4 words per workgroup, to host memory.
+extern "C" int e2sar_hip_debug_trace(int k, uint64_t *out, size_t words)
+{
+    if (k < 0 || k > 1 || words > 8192 * 4) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(e2sar_amd::g_trace), words * 8, (size_t)k * 8192 * 4 * 8,
+                               hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int e2sar_hip_debug_trace_clear(void)
+{
+    static uint64_t zero[2 * 8192 * 4];
+    return hipMemcpyToSymbol(HIP_SYMBOL(e2sar_amd::g_trace), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif

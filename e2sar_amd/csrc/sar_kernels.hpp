@@ -2,6 +2,7 @@
 #pragma once
 
 #include <hip/hip_runtime.h>
+#include <stddef.h>
 #include <stdint.h>
 
 #include "e2sar_hip.h"
@@ -9,19 +10,23 @@
 namespace e2sar_amd {
 
 // In-progress event table entry (the device form of eventsInProgress's
-// shared_ptr<EventQueueItem>, e2sarDPReassembler.hpp:61-99, 224-233).  64 bytes.
+// shared_ptr<EventQueueItem>, e2sarDPReassembler.hpp:61-99, 224-233).  64 bytes, in two
+// 16-byte records a lookup reads in one round trip: A = {state, dataId, eventNum}, written
+// by one 16-byte store when the slot is published, and B = {bufOff, bytes, bvalid}.
 struct ReasSlot {
     uint32_t state;      // EMPTY / BUSY / READY / DONE / LOST
     uint32_t dataId;
-    uint32_t bytes;      // bufferLength of the packet that created the event
-    uint32_t pad0;
     uint64_t eventNum;
-    unsigned long long acc;  // curBytes (low 36 bits) | numFragments (high 28 bits)
     uint64_t bufOff;     // arena offset of the event buffer
+    uint32_t bytes;      // bufferLength of the packet that created the event
+    uint32_t bvalid;     // 1 once bufOff/bytes are written
+    unsigned long long acc;  // curBytes (low 36 bits) | numFragments (high 28 bits)
     uint64_t created;    // firstSegment, caller clock in ms
     uint64_t pad1[2];
 };
 static_assert(sizeof(ReasSlot) == 64, "slot is one 64-byte line");
+static_assert(offsetof(ReasSlot, eventNum) == 8 && offsetof(ReasSlot, bufOff) == 16 && offsetof(ReasSlot, bvalid) == 28,
+              "records A and B are the two first 16-byte quarters of the slot");
 
 constexpr uint32_t kAccFragShift = 36;
 constexpr uint64_t kAccBytesMask = (1ull << kAccFragShift) - 1ull;
@@ -42,7 +47,9 @@ struct ReasCtl {
     uint32_t compactUsed;            // slots claimed in the destination table
     uint32_t pad0;
     uint64_t pad[2];
+    uint64_t pad2[21];
 };
+static_assert(sizeof(ReasCtl) % 128 == 0, "shards follow the control block on 128-byte lines");
 
 // Per-packet counters are sharded (one 128-byte line per shard, shard = block % kShards)
 // so thousands of waves do not serialise on one address; the host sums the shards.

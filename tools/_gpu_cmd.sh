@@ -1,7 +1,7 @@
-mkdir -p gpurun_out/perf2
-timeout -k 10 300 python -m pytest tests/test_dataplane_gpu.py -x -q > gpurun_out/perf2/tests.log 2>&1 || { tail -30 gpurun_out/perf2/tests.log; exit 1; }
-tail -1 gpurun_out/perf2/tests.log
-for r in 5 10 20; do
-timeout -k 10 120 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m 9000 --rate $r > gpurun_out/perf2/lo_9000_r$r.log 2>&1; echo "rc=$?" >> gpurun_out/perf2/lo_9000_r$r.log
-done
-timeout -k 10 120 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m 1500 --rate 5 > gpurun_out/perf2/lo_1500_r5.log 2>&1; echo "rc=$?" >> gpurun_out/perf2/lo_1500_r5.log
+set -e
+O=gpurun_out/chk3; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -60 $O/pytest_gpu.log; exit 1; }
+tail -1 $O/pytest_gpu.log
+timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err
+python -c "import json;d=json.load(open('$O/bench.json'));print(d['value'],d['roofline'])"
+timeout -k 10 200 python tools/ub_concurrency.py > $O/conc.json; cat $O/conc.json

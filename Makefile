@@ -52,3 +52,11 @@ build/e2sar_perf: tools/e2sar_perf.cpp $(HOST_HDRS) include/e2sar_amd/e2sarHeade
 		-Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
 
 all: build/e2sar_perf
+
+# ---- e2sar_ft-shaped file transfer tool over the C++ facade ----
+build/e2sar_ft: tools/e2sar_ft.cpp $(HOST_HDRS) $(LIBDIR)/libe2sar_amd.so
+	@mkdir -p build
+	$(CXX) $(CXXFLAGS) -Iinclude -o $@ tools/e2sar_ft.cpp -L$(LIBDIR) -le2sar_amd -le2sar_hip \
+		-Wl,-rpath,'$$ORIGIN/../$(LIBDIR)' -lpthread
+
+all: build/e2sar_ft

@@ -21,6 +21,7 @@
 #include <random>
 #include <thread>
 
+#include "e2sar_amd/e2sarHeaders.hpp"
 #include "host_common.hpp"
 
 namespace e2sar {
@@ -65,6 +66,18 @@ struct Segmenter::Impl {
     std::atomic<E2SARErrorc> lastErr{E2SARErrorc::NoError};
     std::atomic<EventNum_t> userEventNum{0};
 
+    // Sync thread (useCP): a SyncHdr to the URI's sync address every syncPeriodMs
+    // (e2sarDPSegmenter.cpp:242-373, fillSyncHdr hpp:583-591)
+    int syncFd = -1;
+    sockaddr_storage syncDst{};
+    socklen_t syncDstLen = 0;
+    std::thread syncThread;
+    std::mutex syncMu;
+    std::condition_variable syncCv;
+    bool syncStop = false;
+    std::atomic<uint64_t> syncMsgCnt{0}, syncErrCnt{0};
+    std::atomic<int> syncLastErrno{0};
+
     // send queue (lock-free queue of 2047 items in the reference, hpp:81,101)
     struct Item {
         uint8_t *event;
@@ -96,10 +109,15 @@ struct Segmenter::Impl {
     result<int> ensure(size_t eventBytes, size_t nEvents, size_t nPackets);
     result<int> sendBatch(std::vector<Item> &items);
     void threadBody();
+    result<int> syncOpen();
+    void syncSend();
+    void syncBody();
+    void syncHalt();
 };
 
 Segmenter::Impl::~Impl()
 {
+    syncHalt();
     for (int fd : fds) close(fd);
     if (ctx) {
         e2sar_hip_stream_sync(ctx, stream);
@@ -329,13 +347,104 @@ void Segmenter::Impl::threadBody()
     }
 }
 
-// cpp:160-191 minus the Sync thread; sockets as in cpp:470-657
+// SyncThreadState::_open (e2sarDPSegmenter.cpp:282-337): a UDP socket to the URI's sync
+// address, connected unless connectedSocket is false
+result<int> Segmenter::Impl::syncOpen()
+{
+    auto sa = uri.get_syncAddr();
+    if (sa.has_error()) return sa.error();
+    const std::string &host = sa.value().first;
+    const bool v6 = host.find(':') != std::string::npos;
+    syncDst = sockaddr_storage{};
+    int ok;
+    if (v6) {
+        auto *a = reinterpret_cast<sockaddr_in6 *>(&syncDst);
+        a->sin6_family = AF_INET6;
+        a->sin6_port = htons(sa.value().second);
+        ok = inet_pton(AF_INET6, host.c_str(), &a->sin6_addr);
+        syncDstLen = sizeof(sockaddr_in6);
+    } else {
+        auto *a = reinterpret_cast<sockaddr_in *>(&syncDst);
+        a->sin_family = AF_INET;
+        a->sin_port = htons(sa.value().second);
+        ok = inet_pton(AF_INET, host.c_str(), &a->sin_addr);
+        syncDstLen = sizeof(sockaddr_in);
+    }
+    if (ok != 1) return E2SARErrorInfo{E2SARErrorc::ParameterError, "bad sync address " + host};
+    syncFd = socket(v6 ? AF_INET6 : AF_INET, SOCK_DGRAM, 0);
+    if (syncFd < 0 ||
+        (flags.connectedSocket && connect(syncFd, reinterpret_cast<sockaddr *>(&syncDst), syncDstLen) != 0)) {
+        syncErrCnt++;
+        syncLastErrno = errno;
+        if (syncFd >= 0) close(syncFd);
+        syncFd = -1;
+        return E2SARErrorInfo{E2SARErrorc::SocketError, strerror(syncLastErrno.load())};
+    }
+    return 0;
+}
+
+// fillSyncHdr (hpp:583-591) + _send (cpp:345-373): the reported event number is the wall
+// clock in microseconds (the LB tick the data path stamps), the rate a constant 1 MHz,
+// the time the wall clock in nanoseconds
+void Segmenter::Impl::syncSend()
+{
+    const uint64_t nowNs = (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                               std::chrono::system_clock::now().time_since_epoch())
+                               .count();
+    SyncHdr hdr{};
+    hdr.set(eventSrcId, detail::now_us(), 1000000u, nowNs);
+    syncMsgCnt++;
+    const ssize_t r = flags.connectedSocket
+                          ? send(syncFd, &hdr, sizeof(hdr), 0)
+                          : sendto(syncFd, &hdr, sizeof(hdr), 0, reinterpret_cast<sockaddr *>(&syncDst), syncDstLen);
+    if (r < 0) {
+        syncErrCnt++;
+        syncLastErrno = errno;
+    }
+}
+
+// SyncThreadState::_threadBody (cpp:242-280): one SyncHdr per syncPeriodMs, start to start
+void Segmenter::Impl::syncBody()
+{
+    auto next = std::chrono::steady_clock::now();
+    std::unique_lock<std::mutex> lk(syncMu);
+    while (!syncStop) {
+        lk.unlock();
+        syncSend();
+        lk.lock();
+        next += std::chrono::milliseconds(flags.syncPeriodMs);
+        syncCv.wait_until(lk, next, [&] { return syncStop; });
+    }
+}
+
+void Segmenter::Impl::syncHalt()
+{
+    {
+        std::lock_guard<std::mutex> lk(syncMu);
+        syncStop = true;
+    }
+    syncCv.notify_all();
+    if (syncThread.joinable()) syncThread.join();
+    if (syncFd >= 0) close(syncFd);     // _close (cpp:279, 339-343)
+    syncFd = -1;
+}
+
+// cpp:160-191 (the Sync thread and its warm-up first, as there); sockets as in cpp:470-657
 result<int> Segmenter::openAndStart() noexcept
 {
     auto &m = *impl;
     if (m.started) return 0;
     auto addr = m.useV6 ? m.uri.get_dataAddrv6() : m.uri.get_dataAddrv4();
     if (addr.has_error()) return addr.error();
+    if (m.flags.useCP && !m.syncThread.joinable()) {
+        auto so = m.syncOpen();
+        if (so.has_error())
+            return E2SARErrorInfo{E2SARErrorc::SocketError, "Unable to open sync socket: " + so.error().message()};
+        m.syncStop = false;
+        m.syncThread = std::thread([&m] { m.syncBody(); });
+        // a warm-up period of Sync packets and no data (cpp:174-175)
+        std::this_thread::sleep_for(std::chrono::milliseconds(m.flags.warmUpMs));
+    }
     std::uniform_int_distribution<int> portDist(10000, 65535);
     for (size_t i = 0; i < m.flags.numSendSockets; i++) {
         sockaddr_storage ss{};
@@ -434,7 +543,8 @@ const Segmenter::ReportedStats Segmenter::getSendStats() const noexcept
 
 const Segmenter::ReportedStats Segmenter::getSyncStats() const noexcept
 {
-    return ReportedStats{0, 0, 0, E2SARErrorc::NoError};   // no Sync packets on this path
+    return ReportedStats{impl->syncMsgCnt.load(), impl->syncErrCnt.load(), impl->syncLastErrno.load(),
+                         E2SARErrorc::NoError};
 }
 
 const std::string Segmenter::getIntf() const noexcept { return std::string(); }
@@ -446,6 +556,7 @@ bool Segmenter::isUsingIPv6() const noexcept { return impl->useV6; }
 void Segmenter::stopThreads()
 {
     auto &m = *impl;
+    m.syncHalt();
     if (!m.started) return;
     {
         std::unique_lock<std::mutex> lk(m.qMu);

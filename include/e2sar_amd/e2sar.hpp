@@ -14,8 +14,9 @@
 //   - boost::any callback arguments are std::any; boost::tuple results are std::tuple;
 //     ip::address arguments are std::string.  Outcome's result<T> is a small local type
 //     with the same value()/error()/has_error()/has_value() surface.
-//   - No Sync packets and no control plane (useCP only selects the reference's sanity
-//     checks); registerWorker/deregisterWorker are no-ops that return 0 when !useCP.
+//   - No control plane: with useCP the Segmenter runs the reference's Sync thread (a
+//     SyncHdr to the URI's sync address every syncPeriodMs, after a warmUpMs warm-up) but
+//     talks to no load balancer; registerWorker/deregisterWorker are no-ops that return 0.
 //   - SegmenterFlags/ReassemblerFlags gain device fields (gpuDevice, batch sizes, arena).
 #pragma once
 

@@ -353,3 +353,76 @@ def test_e2sar_perf_tool_loopback():
     assert r.returncode == 0, r.stdout + r.stderr
     assert "50 of 50 events intact" in r.stdout
     assert "eventSuccess=50" in r.stdout and "badHeaderDiscards=0" in r.stdout
+
+
+@pytest.mark.gpu
+def test_sync_thread_frames(E):
+    # DPSyncTest1 (test/e2sar_sync_test.cpp:25-64) and the sync half of DPSegTest1
+    # (e2sar_seg_test.cpp:83-93), scaled from 1 s to 50 ms periods: with useCP the
+    # Segmenter sends a 28-byte SyncHdr (e2sarHeaders.hpp:323-403) to the URI's sync
+    # address every syncPeriodMs, starting with a warm-up before any data
+    import struct
+    sport, dport = next_port(), next_port()
+    cap = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    cap.bind((DP, sport))
+    cap.settimeout(0.2)
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync={DP}:{sport}&data={DP}:{dport}",
+                     E.EjfatURI.TokenType.instance)
+    f = E.DataPlane.Segmenter.SegmenterFlags()
+    f.useCP = True
+    f.syncPeriodMs = 50
+    f.warmUpMs = 100
+    seg = E.DataPlane.Segmenter(uri, DATA_ID, EVENTSRC_ID, f)
+    t0 = time.time_ns()
+    ok(seg.OpenAndStart())
+    assert time.time_ns() - t0 >= 100_000_000            # the warm-up happens inside OpenAndStart
+    time.sleep(0.5)
+    seg.stopThreads()
+    t1 = time.time_ns()
+    st = seg.getSyncStats()
+    frames = []
+    try:
+        while True:
+            frames.append(cap.recv(100))
+    except socket.timeout:
+        pass
+    cap.close()
+    assert st.errCnt == 0
+    assert 9 <= st.msgCnt <= 16, st.msgCnt               # ~0.6 s / 50 ms
+    assert len(frames) == st.msgCnt
+    prev = (0, 0)
+    for fr in frames:
+        assert len(fr) == 28
+        pre, ver, rsvd, esid, evn, rate, tns = struct.unpack(">2sBBIQIQ", fr)
+        assert (pre, ver, rsvd, esid, rate) == (b"LC", 2, 0, EVENTSRC_ID, 1000000)
+        assert t0 <= tns <= t1
+        assert abs(evn - tns // 1000) < 1000             # eventNumber: the clock in microseconds
+        assert (evn, tns) > prev
+        prev = (evn, tns)
+
+
+@pytest.mark.gpu
+def test_e2sar_ft_tool_loopback(tmp_path):
+    # the e2sar_ft-shaped tool (tools/e2sar_ft.cpp, bin/e2sar_ft.cpp): every file matching
+    # the extension becomes one event (mmap -> addToSendQueue -> seg_kernel -> UDP ->
+    # reas_kernel -> recvEvent) and is written back as <prefix>_<event>_<dataId><ext>
+    import subprocess
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "build", "e2sar_ft")
+    if not os.path.exists(exe):
+        pytest.fail("build/e2sar_ft missing: run make")
+    src, out = tmp_path / "in", tmp_path / "out"
+    src.mkdir()
+    out.mkdir()
+    rng = np.random.default_rng(11)
+    sizes = [1, 67, 1436, 1437, 100_000, (1 << 20) + 3]
+    names = [f"f{k}.dat" for k in range(len(sizes))]
+    for n, s in zip(names, sizes):
+        (src / n).write_bytes(rng.integers(0, 256, s, dtype=np.uint8).tobytes())
+    (src / "skip.txt").write_bytes(b"not sent")
+    r = subprocess.run([exe, "--loopback", "-p", str(out), "--port", str(next_port()), "-e", ".dat",
+                        "--dataid", "4321", "-m", "9000", str(src)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    got = sorted(p.name for p in out.iterdir())
+    assert got == sorted(f"e2sar_out_{k}_4321.dat" for k in range(len(sizes)))
+    for k, n in enumerate(sorted(names)):
+        assert (out / f"e2sar_out_{k}_4321.dat").read_bytes() == (src / n).read_bytes(), n

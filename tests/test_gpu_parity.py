@@ -326,6 +326,24 @@ def test_reas_multiple_data_ids_same_event_numbers(hip, reas_mode):
     assert len(got) == 8
 
 
+def test_reas_small_table_collisions(hip, reas_mode):
+    # 48 events in flight in a 64-slot table: long probe chains, slots claimed by one key
+    # while lanes of the same wave with other keys probe past them, the same key in several
+    # runs of one wave (shuffled tails), and events created and completed across batches
+    evs, pk, ln = _events_stream(48, 3000, 80, seed=91)       # maxPld 16: 188 datagrams each
+    per = O.num_packets(3000, O.max_pld_len(80))
+    firsts = [k * per for k in range(48)]
+    rest = [i for i in range(len(ln)) if i % per]
+    random.Random(9).shuffle(rest)
+    order = firsts + rest
+    pk, ln = pk[order], ln[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    for batches in (1, 5):
+        got, st, _ = _reas_gpu(hip, pk, ln, True, batches=batches, table=64, mode=reas_mode)
+        _check_reas(got, st, ref, rst)
+        assert len(got) == 48 and st.errorFlags == 0
+
+
 def test_reas_queue_and_arena_limits(hip, reas_mode):
     # arena too small for all events: the overflow is an enqueue loss, never a fault
     evs, pk, ln = _events_stream(6, 100000, 1500, seed=61)

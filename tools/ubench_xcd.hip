@@ -65,6 +65,36 @@ __global__ __launch_bounds__(256) void copy_static(const uint8_t *src, uint8_t *
     }
 }
 
+// default-policy (or nt) copy with per-workgroup XCD timing: read what the previous kernel wrote
+template <bool NTLD, bool NTST>
+__global__ __launch_bounds__(256) void copy_static_pol(const uint8_t *src, uint8_t *dst, uint64_t nch, uint64_t *trace)
+{
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    const uint64_t c0 = (uint64_t)blockIdx.x * 1024;
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t i = c0 + (uint64_t)u * 256 + threadIdx.x;
+        if (i < nch) v[u] = NTLD ? __builtin_nontemporal_load((const G u32x4 *)(src + 16 * i)) : *(const G u32x4 *)(src + 16 * i);
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+        const uint64_t i = c0 + (uint64_t)u * 256 + threadIdx.x;
+        if (i < nch) {
+            if (NTST) __builtin_nontemporal_store(v[u], (G u32x4 *)(dst + 16 * i));
+            else *(G u32x4 *)(dst + 16 * i) = v[u];
+        }
+    }
+    if (trace) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            trace[2 * blockIdx.x] = ((uint64_t)xcc_id() << 60) | t0;
+            trace[2 * blockIdx.x + 1] = __builtin_amdgcn_s_memrealtime();
+        }
+    }
+}
+
 constexpr uint32_t kUnitRounds = 4;   // 64 KiB per unit
 
 __global__ __launch_bounds__(256) void copy_dyn1(const uint8_t *src, uint8_t *dst, uint64_t nch, uint32_t nUnits,
@@ -167,6 +197,41 @@ int main(int argc, char **argv)
         std::sort(v.begin(), v.end());
         printf("%s%.2f", x ? ", " : "", v.empty() ? 0.0 : v[v.size() / 2]);
     }
-    printf("]}\n");
+    printf("]");
+    // chain: A -> B (default stores), then B -> C timed per XCD: fresh data in the
+    // Infinity Cache, as when reas_kernel reads what seg_kernel just wrote
+    uint8_t *C;
+    CHECK(hipMalloc(&C, bytes));
+    auto per_xcc = [&](const char *name) {
+        CHECK(hipMemcpy(t.data(), trace, t.size() * 8, hipMemcpyDeviceToHost));
+        std::vector<std::vector<double>> dd(16);
+        uint64_t tmin = ~0ull, tmax = 0;
+        for (uint32_t b = 0; b < nStatic; b++) {
+            const uint64_t s0 = t[2 * b] & ((1ull << 60) - 1);
+            dd[(t[2 * b] >> 60) & 15].push_back((double)(t[2 * b + 1] - s0) * 0.01);
+            tmin = std::min(tmin, s0);
+            tmax = std::max(tmax, t[2 * b + 1]);
+        }
+        printf(", \"%s_span_us\": %.1f, \"%s_by_xcc\": [", name, (tmax - tmin) * 0.01, name);
+        for (int x = 0; x < 8; x++) {
+            auto &v = dd[x];
+            std::sort(v.begin(), v.end());
+            printf("%s%.2f", x ? ", " : "", v.empty() ? 0.0 : v[v.size() / 2]);
+        }
+        printf("]");
+    };
+    for (int rep = 0; rep < 3; rep++) {
+        copy_static_pol<true, false><<<nStatic, 256>>>(src, dst, nch, nullptr);
+        copy_static_pol<false, true><<<nStatic, 256>>>(dst, C, nch, trace);
+    }
+    CHECK(hipDeviceSynchronize());
+    per_xcc("fresh_read");
+    for (int rep = 0; rep < 3; rep++) {
+        copy_static_pol<true, true><<<nStatic, 256>>>(src, dst, nch, nullptr);
+        copy_static_pol<false, true><<<nStatic, 256>>>(dst, C, nch, trace);
+    }
+    CHECK(hipDeviceSynchronize());
+    per_xcc("after_nt_write");
+    printf("}\n");
     return 0;
 }

@@ -3,9 +3,10 @@
 
 One step = every event of this rank's working set (default 1024 x 1 MiB) is segmented
 into LB+RE datagrams (MTU 1500 -> 731 per event) and the datagrams are reassembled
-into a fresh event arena, batch by batch (default 128 events = 93,568 datagrams =
-188 MB per batch, so a batch's datagrams can stay in the 256 MiB Infinity Cache between
-the two kernels; tools/ab_batch.sh: 64 -> 1125 GiB/s, 128 -> 1283, 256 -> 1181).  Inputs (event bytes + the 40-byte-per-event descriptor tables) are resident
+into a fresh event arena, batch by batch (default 205 events = 149,855 datagrams =
+221 MB of datagram slots per batch, so a batch's datagrams can stay in the 256 MiB
+Infinity Cache between the two kernels; A/B: 128 -> 1295 GiB/s, 192 -> 1331,
+205 -> 1351, 228 -> 1314, 256 -> 1187).  Inputs (event bytes + the 40-byte-per-event descriptor tables) are resident
 in HBM before timing starts.  N>1: one process per GPU (torch.distributed.run), events
 sharded by eventNum % world (weak scaling, no data-path collective).
 
@@ -34,8 +35,9 @@ def parse():
     ap.add_argument("--mtu", type=int, default=1500)
     ap.add_argument("--event-bytes", type=int, default=1 << 20)
     ap.add_argument("--events", type=int, default=1024, help="events per rank per step")
-    ap.add_argument("--batch-events", type=int, default=128,
-                    help="events per segment/reassemble launch (128 x 1 MiB: 94K datagrams, 188 MB, fits the 256 MiB Infinity Cache)")
+    ap.add_argument("--batch-events", type=int, default=205,
+                    help="events per segment/reassemble launch (205 x 1 MiB: 150K datagrams, 221 MB: five "
+                         "launches per 1024-event step whose datagram batch still fits the 256 MiB Infinity Cache)")
     ap.add_argument("--lb-version", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
     ap.add_argument("--no-verify", action="store_true")

@@ -35,6 +35,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_U
 #define E2SAR_REAS_U 4
 #endif
+#ifndef E2SAR_SEG_U
+#define E2SAR_SEG_U 4               // 16-byte output chunks per thread of seg_kernel
+#endif
 #ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
 #define E2SAR_REAS_CHUNKS_PER_BLOCK 9216u
 #endif
@@ -1150,7 +1153,7 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream)
 {
-    constexpr int U = 4;
+    constexpr int U = E2SAR_SEG_U;
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
     if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32

@@ -28,6 +28,11 @@ inline uint64_t now_us()
         .count();
 }
 
+// clockEntropyTest (e2sarUtil.hpp:549-574): Shannon entropy, in bits, of the low 8 bits of
+// the microsecond wall clock sampled every sleepMs; measured once per process (the clock
+// does not change under it) -- the reference measures it in every Segmenter constructor
+float clock_entropy_bits();
+
 inline uint64_t steady_ms()
 {
     return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(

@@ -28,6 +28,8 @@ namespace e2sar {
 
 using detail::hip_error;
 
+constexpr float kMinClockEntropy = 6.0f;   // MIN_CLOCK_ENTROPY (e2sarDPSegmenter.hpp:293)
+
 struct Segmenter::Impl {
     EjfatURI uri;
     uint16_t dataId;
@@ -97,6 +99,7 @@ struct Segmenter::Impl {
     std::atomic<bool> stop{false};
     bool started = false;
     std::mt19937 rng{std::random_device{}()};
+    bool addEntropy = false;                              // clock LSBs need help (cpp:50)
     std::chrono::steady_clock::time_point paceNext{};   // rate pacing: earliest start of the next event
 
     Impl(const EjfatURI &u, uint16_t did, uint32_t esid, std::vector<int> c, const SegmenterFlags &f)
@@ -154,6 +157,7 @@ static void init_impl(Segmenter::Impl &m)
     m.mtu = m.flags.mtu ? m.flags.mtu : 1500;   // mtu 0 (netlink auto-detect) -> 1500 here
     m.sanity();
     m.maxPld = e2sar_hip_max_pld_len(m.mtu, m.useV6 ? 1 : 0);     // cpp:113
+    m.addEntropy = !(detail::clock_entropy_bits() > kMinClockEntropy);   // cpp:50
     m.stride = e2sar_hip_packet_stride(m.maxPld);
     int rc = e2sar_hip_stream_create(m.flags.gpuDevice, &m.stream);
     if (rc == 0) rc = e2sar_hip_ctx_create(m.flags.gpuDevice, m.stream, &m.ctx);
@@ -242,8 +246,10 @@ result<int> Segmenter::Impl::sendBatch(std::vector<Item> &items)
             return hip_error(rc, "event copy to device");
         auto &d = hDesc[i];
         d.data = dEvents + off;
-        // lbEventNum = wall clock in microseconds (cpp:707-719); entropy 0 => random (cpp:727-728)
-        d.lbTick = detail::now_us();
+        // lbEventNum = wall clock in microseconds, its low 8 bits random when the clock has
+        // too little entropy there (cpp:707-719, addClockEntropy hpp:600-603); entropy 0 =>
+        // random (cpp:727-728)
+        d.lbTick = addEntropy ? ((detail::now_us() & ~uint64_t(0xFF)) | (rng() & 0xFFu)) : detail::now_us();
         d.eventNum = flags.ticksAsREEventNum ? d.lbTick : items[i].eventNum;   // cpp:723-724
         d.dataId = items[i].dataId;
         d.entropy = items[i].entropy ? items[i].entropy : (uint16_t)(rng() & 0xFFFF);

@@ -1,6 +1,11 @@
 // util.cpp -- EjfatURI (data-path subset), get_PortRange, INI flag loading.
 #include <algorithm>
 #include <cctype>
+#include <chrono>
+#include <cmath>
+#include <mutex>
+#include <thread>
+#include <vector>
 #include <cerrno>
 #include <cstdlib>
 #include <cstring>
@@ -96,6 +101,29 @@ int get_PortRange(int source_count) noexcept
 }
 
 namespace detail {
+
+float clock_entropy_bits()
+{
+    static std::once_flag once;
+    static float bits = 0.0f;
+    std::call_once(once, [] {
+        constexpr int kTests = 1000;
+        std::vector<int> bins(256, 0);
+        for (int i = 0; i < kTests; i++) {
+            const auto now = std::chrono::system_clock::now();
+            bins[std::chrono::duration_cast<std::chrono::microseconds>(now.time_since_epoch()).count() & 0xff]++;
+            std::this_thread::sleep_until(now + std::chrono::milliseconds(1));
+        }
+        double e = 0.0;
+        for (int b : bins)
+            if (b) {
+                const double p = (double)b / kTests;
+                e -= p * std::log(p);
+            }
+        bits = (float)(e / std::log(2.0));
+    });
+    return bits;
+}
 
 static std::string trim(const std::string &s)
 {

@@ -1,4 +1,4 @@
 set -e
-O=gpurun_out/segu; mkdir -p $O
-tools/ab_variants.sh segu "--steps 20" base s2 s6 s8 base s8
-for v in base s2 s6 s8; do python -c "import json;d=json.load(open('$O/$v.json'));print('$v',d['value'],d['roofline']['avg_launch_ms'])"; done
+O=gpurun_out/ent; mkdir -p $O
+timeout -k 10 600 python -u -m pytest tests/test_dataplane_gpu.py -x -v --timeout 120 --timeout-method thread > $O/pytest.log 2>&1 || { tail -40 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log

@@ -426,3 +426,43 @@ def test_e2sar_ft_tool_loopback(tmp_path):
     assert got == sorted(f"e2sar_out_{k}_4321.dat" for k in range(len(sizes)))
     for k, n in enumerate(sorted(names)):
         assert (out / f"e2sar_out_{k}_4321.dat").read_bytes() == (src / n).read_bytes(), n
+
+
+@pytest.mark.gpu
+def test_ipv6_loopback(E):
+    # dpV6: IPv6 data address from the URI, maxPldLen = mtu - 84 (e2sarHeaders.hpp:415-421),
+    # datagrams over ::1 reassembled bit-exactly
+    try:
+        probe = socket.socket(socket.AF_INET6, socket.SOCK_DGRAM)
+        probe.bind(("::1", 0))
+        probe.close()
+    except OSError:
+        pytest.skip("no IPv6 loopback on this host")
+    port = next_port()
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?data=[::1]:{port}", E.EjfatURI.TokenType.instance)
+    sf = E.DataPlane.Segmenter.SegmenterFlags()
+    sf.useCP = False
+    sf.dpV6 = True
+    seg = E.DataPlane.Segmenter(uri, DATA_ID, EVENTSRC_ID, sf)
+    assert seg.getMaxPldLen() == 1500 - 84
+    rf = E.DataPlane.Reassembler.ReassemblerFlags()
+    rf.useCP = False
+    rf.withLBHeader = True
+    rf.arenaBytes = 64 << 20
+    reas = E.DataPlane.Reassembler(uri, E.IPAddress.from_string("::1"), port, 1, rf)
+    ok(reas.OpenAndStart())
+    ok(seg.OpenAndStart())
+    rng = np.random.default_rng(17)
+    evs = [rng.integers(0, 256, s, dtype=np.uint8) for s in (1, 1416, 1417, 70000, 1 << 20)]
+    for k, e in enumerate(evs):
+        ok(seg.addNumpyArrayToSendQueue(e, e.nbytes, 100 + k))
+    got = {}
+    while len(got) < len(evs):
+        n, out, ev, did = reas.recv1DNumpyArray(np.uint8().dtype, 10000)
+        assert n > 0, reas.getStats().reassemblyLoss
+        got[ev] = out
+    seg.stopThreads()
+    reas.stopThreads()
+    for k, e in enumerate(evs):
+        assert np.array_equal(got[100 + k], e)
+    assert seg.getSendStats().msgCnt == sum(O.num_packets(e.nbytes, 1416) for e in evs)

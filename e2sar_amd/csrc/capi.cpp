@@ -266,6 +266,26 @@ int e2sar_hip_segment_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_eve
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_segment_batch_dev(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, const uint32_t *d_counts,
+                                uint32_t maxEvents, uint32_t maxPacketsPerEvent, int lbHdrVersion, uint32_t maxPldLen,
+                                uint8_t *d_packets, uint32_t stride, uint32_t *d_lens, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (maxEvents == 0) return E2SAR_HIP_OK;
+    if (!d_events || !d_counts || !d_packets) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    if (maxPldLen > 65535u) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen above a UDP datagram");
+    if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = launch_segment(d_events, maxEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen,
+                                  maxPldLen % 4u == 0, d_packets, stride, d_lens, s, d_counts);
+    if (e != hipSuccess) return hip_fail(e, "seg_kernel launch");
+    return E2SAR_HIP_OK;
+}
+
 /* ---------------- reassembly ---------------- */
 
 int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, e2sar_hip_reas **out)
@@ -375,6 +395,22 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_relay_plan(e2sar_hip_reas *r, uint32_t firstRecord, uint32_t maxEvents, size_t maxPldLen,
+                         uint64_t lbTick, uint16_t entropyBase, e2sar_hip_seg_event *d_events, uint32_t *d_counts,
+                         void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (!d_events || !d_counts) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (maxPldLen == 0 || maxPldLen > 65535u) return fail(E2SAR_HIP_ERR_PARAMETER, "bad maxPldLen");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_relay_plan(r->dev, firstRecord, maxEvents, (uint32_t)maxPldLen, lbTick, entropyBase,
+                                     d_events, d_counts, s);
+    if (e != hipSuccess) return hip_fail(e, "relay_plan launch");
     return E2SAR_HIP_OK;
 }
 

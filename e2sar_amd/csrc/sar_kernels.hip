@@ -208,15 +208,19 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 // that END at its last dword, then shifts them down in registers) -- and only phase 2
 // consumes them.  So no load result sits behind a branch and all U loads of a lane are
 // in flight together.
+// dCount (optional): the number of events is read on the device (the relay form, whose
+// event table is built by relay_plan_kernel); blocks of events past it exit.
 template <bool A4, int U>
 __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                      uint32_t blocksPerEvent, int lbVersion,
                                                      uint32_t maxPld, uint8_t *__restrict__ pkts,
-                                                     uint32_t stride, uint32_t *__restrict__ lens)
+                                                     uint32_t stride, uint32_t *__restrict__ lens,
+                                                     const uint32_t *__restrict__ dCount)
 {
     TRACE_AT(1, 0, trace_now());
     const uint32_t e = blockIdx.x / blocksPerEvent;
     const uint32_t bx = blockIdx.x - e * blocksPerEvent;
+    if (dCount && e >= *dCount) return;
     const e2sar_hip_seg_event ev = events[e];
     const uint32_t bytes = ev.bytes;
     const uint32_t npk = (bytes + maxPld - 1u) / maxPld;
@@ -1151,7 +1155,7 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
-                          hipStream_t stream)
+                          hipStream_t stream, const uint32_t *d_count)
 {
     constexpr int U = E2SAR_SEG_U;
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
@@ -1162,10 +1166,81 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (aligned4)
         hipLaunchKernelGGL((seg_kernel<true, U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream,
-                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens);
+                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens, d_count);
     else
         hipLaunchKernelGGL((seg_kernel<false, U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream,
-                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens);
+                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens, d_count);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------------
+// relay: the events a reassembler completed become a segmentation batch on the device
+//
+// One workgroup reads completed records [first, first + n) (n = min(maxEvents, records
+// stored - first)), writes one seg descriptor per event -- the event's arena bytes, its RE
+// eventNum and dataId as received, the batch's LB tick, entropy entropyBase + i -- with
+// pktBase the exclusive prefix of ceil(bytes / maxPld) (a block-wide scan, 256 records per
+// step), and counts[0] = n, counts[1] = the batch's datagram count.
+
+__global__ __launch_bounds__(kBlock) void relay_plan_kernel(ReasDev R, uint32_t first, uint32_t maxEvents,
+                                                            uint32_t maxPld, uint64_t lbTick, uint32_t entropyBase,
+                                                            e2sar_hip_seg_event *__restrict__ out,
+                                                            uint32_t *__restrict__ counts)
+{
+    __shared__ uint32_t waveSum[kBlock / 64];
+    __shared__ uint32_t sN;
+    const uint32_t lane = threadIdx.x & 63u, wv = threadIdx.x >> 6;
+    if (threadIdx.x == 0) {
+        uint32_t stored = ld_agent(&R.ctl->nCompleted);
+        if (stored > R.queueCapacity) stored = R.queueCapacity;        // records past it were lost
+        const uint32_t avail = stored > first ? stored - first : 0u;
+        sN = avail < maxEvents ? avail : maxEvents;
+    }
+    __syncthreads();
+    const uint32_t n = sN;
+    uint32_t carry = 0;
+    for (uint32_t b0 = 0; b0 < n; b0 += kBlock) {
+        const uint32_t i = b0 + threadIdx.x;
+        e2sar_hip_event_rec rec{};
+        if (i < n) rec = R.completed[first + i];
+        const uint32_t np = (i < n) ? (rec.bytes + maxPld - 1u) / maxPld : 0u;
+        uint32_t inc = np;                                   // inclusive scan in the wave
+#pragma unroll
+        for (uint32_t o = 1; o < 64; o <<= 1) {
+            const uint32_t y = __shfl_up(inc, o);
+            if (lane >= o) inc += y;
+        }
+        if (lane == 63) waveSum[wv] = inc;
+        __syncthreads();
+        uint32_t before = carry;
+        for (uint32_t w = 0; w < wv; w++) before += waveSum[w];
+        if (i < n) {
+            e2sar_hip_seg_event d;
+            d.data = R.arena + rec.arenaOffset;
+            d.eventNum = rec.eventNum;
+            d.lbTick = lbTick;
+            d.bytes = rec.bytes;
+            d.pktBase = before + inc - np;
+            d.dataId = rec.dataId;
+            d.entropy = (uint16_t)(entropyBase + i);
+            d.reserved = 0;
+            out[i] = d;
+        }
+        for (uint32_t w = 0; w < kBlock / 64; w++) carry += waveSum[w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        counts[0] = n;
+        counts[1] = carry;
+    }
+}
+
+hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvents, uint32_t maxPld,
+                             uint64_t lbTick, uint32_t entropyBase, e2sar_hip_seg_event *d_events,
+                             uint32_t *d_counts, hipStream_t stream)
+{
+    hipLaunchKernelGGL(relay_plan_kernel, dim3(1), dim3(kBlock), 0, stream, R, first, maxEvents, maxPld, lbTick,
+                       entropyBase, d_events, d_counts);
     return hipGetLastError();
 }
 

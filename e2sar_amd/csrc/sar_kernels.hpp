@@ -103,10 +103,14 @@ static_assert(sizeof(FinishRec) == 32, "two dwordx4 per record");
 inline size_t work_fin_off(uint32_t n) { return ((size_t)n * sizeof(PktInfo) + 255) & ~(size_t)255; }
 inline size_t work_bytes(uint32_t n) { return work_fin_off(n) + (size_t)n * sizeof(FinishRec); }
 
+// d_count (optional): the event count is read on the device; nEvents is then its bound
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
-                          hipStream_t stream);
+                          hipStream_t stream, const uint32_t *d_count = nullptr);
+hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvents, uint32_t maxPld,
+                             uint64_t lbTick, uint32_t entropyBase, e2sar_hip_seg_event *d_events,
+                             uint32_t *d_counts, hipStream_t stream);
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,

@@ -144,6 +144,22 @@ class DeviceSegmenter:
             C.c_void_p(_stream_handle(stream))))
         return plan.total_packets
 
+    def segment_device(self, events: torch.Tensor, counts: torch.Tensor, max_events: int,
+                       max_packets_per_event: int, packets: torch.Tensor, lens: Optional[torch.Tensor],
+                       stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Segment a descriptor table built on the device (DeviceReassembler.relay_plan):
+        the event count is counts[0], read by the kernel; max_events bounds it."""
+        if packets.numel() < max_events * max_packets_per_event * self.stride:
+            raise ValueError("packet buffer too small for the bound")
+        check(lib().e2sar_hip_segment_batch_dev(
+            self.ctx.handle, C.c_void_p(events.data_ptr()), C.c_void_p(counts.data_ptr()), max_events,
+            max_packets_per_event, self.lb_hdr_version, self.max_pld, C.c_void_p(packets.data_ptr()),
+            self.stride, C.c_void_p(lens.data_ptr() if lens is not None else 0),
+            C.c_void_p(_stream_handle(stream))))
+
+
+SEG_EVENT_BYTES = 40       # sizeof(e2sar_hip_seg_event)
+
 
 class DeviceReassembler:
     """Reassembles device-resident datagram batches into a device event arena.
@@ -180,6 +196,18 @@ class DeviceReassembler:
         check(lib().e2sar_hip_reassemble_batch(
             self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
             int(now_ms), C.c_void_p(_stream_handle(stream))))
+
+    def relay_plan(self, events: torch.Tensor, counts: torch.Tensor, first_record: int, max_events: int,
+                   max_pld: int, lb_tick: int, entropy_base: int,
+                   stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Completed records [first_record, +n) -> seg descriptors in `events` (uint8 device
+        tensor of max_events * SEG_EVENT_BYTES) and counts[0:2] = (n, datagrams) (int32/uint32
+        device tensor), without a host round trip (e2sar_hip_relay_plan)."""
+        if events.numel() < max_events * SEG_EVENT_BYTES or counts.numel() < 2:
+            raise ValueError("relay buffers too small")
+        check(lib().e2sar_hip_relay_plan(
+            self._h, first_record, max_events, max_pld, int(lb_tick), entropy_base & 0xFFFF,
+            C.c_void_p(events.data_ptr()), C.c_void_p(counts.data_ptr()), C.c_void_p(_stream_handle(stream))))
 
     # ---- split form: classify (headers, table) then scatter (bytes), for pipelining ----
     @staticmethod

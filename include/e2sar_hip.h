@@ -250,6 +250,29 @@ int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream);
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
 
 /* ------------------------------------------------------------------ */
+/* relay (BASELINE config 5: receive -> reassemble -> segment -> send on one GPU): the    */
+/* events a reassembler completed are segmented again without a host round trip.  The  */
+/* Segmenter's per-event rules (numbering, dataId, entropy, LB tick: cpp:707-728,      */
+/* 901-948) are replaced by: RE eventNum and dataId as received, one LB tick for the   */
+/* batch, entropy of the i-th planned event = entropyBase + i (mod 2^16).               */
+
+/* Completed records [firstRecord, firstRecord + n) -- n = min(maxEvents, records the    */
+/* reassembler holds past firstRecord) -- become seg descriptors d_events[0, n) (device, */
+/* maxEvents entries) with pktBase filled in; d_counts[0] = n, d_counts[1] = their       */
+/* datagram count (device, 2 entries).  The event bytes stay in the arena: recycle or    */
+/* compact only after the segmentation that reads them.  Asynchronous.                  */
+int e2sar_hip_relay_plan(e2sar_hip_reas *r, uint32_t firstRecord, uint32_t maxEvents, size_t maxPldLen,
+                         uint64_t lbTick, uint16_t entropyBase, e2sar_hip_seg_event *d_events,
+                         uint32_t *d_counts, void *stream);
+/* e2sar_hip_segment_batch with the event count read on the device (d_counts[0], as     */
+/* e2sar_hip_relay_plan writes it); maxEvents bounds it.  Event data 256-byte aligned    */
+/* (arena buffers), so the dword-aligned path is used when maxPldLen % 4 == 0.           */
+int e2sar_hip_segment_batch_dev(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events,
+                                const uint32_t *d_counts, uint32_t maxEvents, uint32_t maxPacketsPerEvent,
+                                int lbHdrVersion, uint32_t maxPldLen, uint8_t *d_packets, uint32_t stride,
+                                uint32_t *d_lens, void *stream);
+
+/* ------------------------------------------------------------------ */
 /* multi-GPU: events are owned by rank eventNum % world.  A rank that received       */
 /* (landed) datagrams of other ranks' events routes them: this packs the batch into */
 /* per-destination spans (stable order) and reports the span sizes, ready for one   */

@@ -450,3 +450,45 @@ def test_route_batch_matches_stable_route(hip, world, self_rank):
     np.testing.assert_array_equal(sln[:n].cpu().numpy().astype(np.uint32), rln)
     got = spk[: n * stride].cpu().numpy().reshape(n, stride)
     np.testing.assert_array_equal(got, rpk)
+
+
+def test_relay_resegments_completed_events(hip):
+    # BASELINE config 5 on the device: segment -> reassemble -> relay_plan -> segment_device.
+    # Every re-sent datagram equals the oracle's segmentation of the reassembled event with
+    # the relay's rules (RE eventNum and dataId as received, one LB tick, entropy base + i)
+    torch = _torch()
+    from e2sar_amd import sar
+    sizes = [1, 1436, 1437, 3 * 1436 + 5, 100_000, 1 << 20]
+    host = [_rng_bytes(500 + k, s) for k, s in enumerate(sizes)]
+    evs = [(b, 10 + k, 7, 1 + k, 99 + k) for k, b in enumerate(host)]
+    gp, gl, seg = _segment_gpu(hip, evs, 1500, 2)
+    R = sar.DeviceReassembler(hip, with_lb_header=True, arena_bytes=8 << 20)
+    dpk = _dev(gp.reshape(-1), hip)
+    dln = _dev(gl.view(np.int32), hip)
+    R.reassemble(dpk, seg.stride, dln, gp.shape[0])
+    n_ev = len(sizes)
+    mp = O.max_pld_len(1500)
+    max_pk = max(O.num_packets(s, mp) for s in sizes)
+    d_events = torch.zeros(n_ev * sar.SEG_EVENT_BYTES, dtype=torch.uint8, device=hip.torch_device)
+    counts = torch.zeros(2, dtype=torch.int32, device=hip.torch_device)
+    tick = 0x0102030405060708
+    R.relay_plan(d_events, counts, 0, n_ev, mp, tick, 0xFFFE)          # entropy wraps past 0xFFFF
+    out = sar.DeviceSegmenter(hip, mtu=1500, lb_hdr_version=3)
+    opk, oln = out.alloc_packets(n_ev * max_pk)
+    out.segment_device(d_events, counts, n_ev, max_pk, opk, oln)
+    torch.cuda.synchronize()
+    n, total = (int(x) for x in counts.cpu())
+    assert n == n_ev and total == sum(O.num_packets(s, mp) for s in sizes)
+    dt = np.dtype([("data", "<u8"), ("eventNum", "<u8"), ("lbTick", "<u8"), ("bytes", "<u4"), ("pktBase", "<u4"),
+                   ("dataId", "<u2"), ("entropy", "<u2"), ("reserved", "<u4")])
+    desc = d_events.cpu().numpy().view(dt)
+    got_pk = opk[: total * out.stride].view(total, out.stride).cpu().numpy()
+    got_ln = oln[:total].cpu().numpy().astype(np.uint32)
+    assert sorted(int(d["eventNum"]) for d in desc) == [10 + k for k in range(n_ev)]
+    for i, d in enumerate(desc):
+        k = int(d["eventNum"]) - 10
+        assert int(d["bytes"]) == sizes[k] and int(d["dataId"]) == 7 and int(d["lbTick"]) == tick
+        assert int(d["entropy"]) == (0xFFFE + i) & 0xFFFF
+        op, ol = O.segment_event(host[k], 10 + k, 7, (0xFFFE + i) & 0xFFFF, tick, 3, mp, out.stride)
+        b = int(d["pktBase"])
+        _assert_same_datagrams(got_pk[b:b + len(ol)], got_ln[b:b + len(ol)], op, ol)

@@ -4,7 +4,10 @@
 Receive direction: pinned host datagram batches (what recvmmsg fills) -> H2D -> reas_kernel
 -> completed events D2H into pinned host memory (what getEvent hands out).
 Send direction: pinned host events -> H2D -> seg_kernel -> datagrams D2H into pinned host
-memory (what sendmmsg drains).  Each direction runs on two streams -- H2D copy + kernel on
+memory (what sendmmsg drains).  Relay (BASELINE config 5): pinned datagram batches -> H2D ->
+reas_kernel -> relay_plan_kernel + seg_kernel on the reassembled events (no host round trip)
+-> datagrams D2H; the host learns each batch's datagram count from a 8-byte D2H one batch
+behind, so the GPU is never idle waiting for it.  Each direction runs on two streams -- H2D copy + kernel on
 one, D2H copy on the other -- over --slots rotating buffer sets, so the whole process
 uses four streams (GPU_MAX_HW_QUEUES is 4: more streams than hardware queues share
 queues and serialise).  "both" runs the two directions at once (PCIe is full duplex).
@@ -35,7 +38,7 @@ def main():
     ap.add_argument("--batches", type=int, default=64)
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--slots", type=int, default=3)
-    ap.add_argument("--only", choices=["recv", "send", "both"], default=None,
+    ap.add_argument("--only", choices=["recv", "send", "both", "relay"], default=None,
                     help="time one mode only (for tracing)")
     args = ap.parse_args()
 
@@ -119,17 +122,57 @@ def main():
             e2.record(ss[1])
         ev_done[s] = e2
 
+    # relay: datagrams in, the reassembled events segmented again on the device, datagrams out
+    relay_desc = [torch.zeros(BE * sar.SEG_EVENT_BYTES, dtype=torch.uint8, device=dev) for _ in range(S)]
+    relay_cnt = [torch.zeros(2, dtype=torch.int32, device=dev) for _ in range(S)]
+    relay_hcnt = [torch.zeros(2, dtype=torch.int32).pin_memory() for _ in range(S)]
+
+    def relay_front(k, ev_done, ev_cnt):
+        s = k % S
+        with torch.cuda.stream(rs[0]):
+            if ev_done[s] is not None:
+                rs[0].wait_event(ev_done[s])
+            d_pk[s].copy_(h_pk[s], non_blocking=True)
+            d_ln[s].copy_(h_ln[s], non_blocking=True)
+            R[s].recycle(force=True, stream=rs[0])
+            R[s].reassemble(d_pk[s], stride, d_ln[s], bpk, stream=rs[0])
+            R[s].relay_plan(relay_desc[s], relay_cnt[s], 0, BE, seg.max_pld, 7 + k, 1 + k, stream=rs[0])
+            seg.segment_device(relay_desc[s], relay_cnt[s], BE, npk, d_spk[s][0], d_spk[s][1], stream=rs[0])
+            relay_hcnt[s].copy_(relay_cnt[s], non_blocking=True)
+            e1 = torch.cuda.Event()
+            e1.record(rs[0])
+        ev_cnt[s] = e1
+
+    def relay_back(k, ev_done, ev_cnt):
+        s = k % S
+        ev_cnt[s].synchronize()                  # the batch's datagram count, one batch behind
+        total = int(relay_hcnt[s][1])
+        rs[1].wait_event(ev_cnt[s])
+        with torch.cuda.stream(rs[1]):
+            h_out_pk[s][: total * stride].copy_(d_spk[s][0][: total * stride], non_blocking=True)
+            e2 = torch.cuda.Event()
+            e2.record(rs[1])
+        ev_done[s] = e2
+        return total
+
     def run(mode):
         best = 0.0
         for _ in range(args.iters):
             torch.cuda.synchronize()
-            rd, sd = [None] * S, [None] * S
+            rd, sd, rc = [None] * S, [None] * S, [None] * S
             t0 = time.perf_counter()
             for k in range(args.batches):
+                if mode == "relay":
+                    relay_front(k, rd, rc)
+                    if k:
+                        relay_back(k - 1, rd, rc)
+                    continue
                 if mode in ("recv", "both"):
                     recv_batch(k, rd)
                 if mode in ("send", "both"):
                     send_batch(k, sd)
+            if mode == "relay":
+                relay_back(args.batches - 1, rd, rc)
             torch.cuda.synchronize()
             dt = time.perf_counter() - t0
             best = max(best, args.batches * BE * B / dt / 2**30)
@@ -151,8 +194,14 @@ def main():
         res[args.only + "_GiBps"] = round(run(args.only), 2)
         print(json.dumps(res), flush=True)
         return
+    # correctness of the relay: one batch through, the re-sent datagrams carry every event
+    rd, rc = [None] * S, [None] * S
+    relay_front(0, rd, rc)
+    total = relay_back(0, rd, rc)
+    torch.cuda.synchronize()
+    assert total == bpk, (total, bpk)
     res.update({"recv_GiBps": round(run("recv"), 2), "send_GiBps": round(run("send"), 2),
-                "both_GiBps_each_direction": round(run("both"), 2)})
+                "both_GiBps_each_direction": round(run("both"), 2), "relay_GiBps": round(run("relay"), 2)})
     # PCIe alone: the same copies without kernels
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -40,6 +40,9 @@ def parse():
                          "launches per 1024-event step whose datagram batch still fits the 256 MiB Infinity Cache)")
     ap.add_argument("--lb-version", type=int, default=2)
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--payload", choices=["random", "perf"], default="random",
+                    help="random: seeded uniform bytes; perf: e2sar_perf's event (head 'This is a start of "
+                         "event payload', tail '...the end', bin/e2sar_perf.cpp:27-28,153-154; zeros between)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
@@ -167,6 +170,12 @@ def main():
     g.manual_seed(0xE25A2 + rank)
     ev_stride = (B + 255) // 256 * 256
     src = torch.randint(0, 256, (E, ev_stride), dtype=torch.uint8, device=dev, generator=g)
+    if args.payload == "perf":
+        head, tail = b"This is a start of event payload", b"...the end"
+        assert B >= len(head) + len(tail)
+        src.zero_()
+        src[:, :len(head)] = torch.tensor(list(head), dtype=torch.uint8, device=dev)
+        src[:, B - len(tail):B] = torch.tensor(list(tail), dtype=torch.uint8, device=dev)
     if args.landing == "own":
         evnum = lambda i: i * world + rank      # every local event is owned here: eventNum % world == rank
     else:
@@ -442,7 +451,8 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (torch Philox uniform bytes, seeded per rank)",
+            "data": ("synthetic (torch Philox uniform bytes, seeded per rank)" if args.payload == "random" else
+                     "synthetic (e2sar_perf event pattern: head + tail strings, zeros between)"),
             "config": {
                 "workload": (f"{E} x {B} B events/rank/step, MTU {args.mtu} (maxPld {mp}, {npk} datagrams/event), "
                              f"LB v{args.lb_version} + RE headers, withLBHeader, {args.batch_events} events per "
@@ -456,6 +466,7 @@ def main():
                                "pipelined": "reas_scatter_classify_kernel: scatter(b) beside classify(b+1), "
                                             "2 datagram buffers"}[args.reas],
                 "landing": args.landing,
+                "payload": args.payload,
                 "verified_roundtrip": verified,
             },
             "roofline": {

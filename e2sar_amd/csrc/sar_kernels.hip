@@ -26,6 +26,7 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
+
 // Occupancy cap of the fused reassembly kernel (0 = whatever its registers allow).
 #ifndef E2SAR_REAS_WAVES
 #define E2SAR_REAS_WAVES 0
@@ -51,11 +52,19 @@ constexpr int kBlock = 256;
 #define E2SAR_TRACE 0
 #endif
 #if E2SAR_TRACE
-__device__ uint64_t g_trace[2][8192 * 4];
+__device__ uint64_t g_trace[3][8192 * 4];
 #define TRACE_AT(k, slot, i) \
     do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
+// by the first active lane of wave 0 (inside divergent code)
+#define TRACE_FIRST(k, slot, i) \
+    do { if (threadIdx.x < 64 && blockIdx.x < 8192 && \
+             threadIdx.x == (uint32_t)(__builtin_ffsll((long long)__ballot(1)) - 1)) \
+             g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
+#define TRACE_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 #else
 #define TRACE_AT(k, slot, i) do {} while (0)
+#define TRACE_FIRST(k, slot, i) do {} while (0)
+#define TRACE_WAIT() do {} while (0)
 #endif
 __device__ __forceinline__ uint64_t trace_now() { return __builtin_amdgcn_s_memrealtime(); }
 __device__ __forceinline__ uint64_t trace_hwid()
@@ -396,11 +405,20 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
     uint32_t h = slot_hash(ev, d, mask);
     uint32_t probes = 0, spins = 0;
     bool active = want;
+#if E2SAR_TRACE
+    uint32_t pass = 0;
+#endif
     while (__ballot(active)) {
         bool waiting = false, advance = false;
         if (active) {
             ReasSlot *sl = R.slots + h;
             const uint32_t old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+#if E2SAR_TRACE
+            if (pass == 0) {
+                TRACE_WAIT();
+                TRACE_FIRST(2, 1, trace_now());
+            }
+#endif
             if (old == kEmpty) {
                 // this lane owns the slot: buffer, then records B and A
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
@@ -451,7 +469,16 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             }
         }
         if (__ballot(waiting)) __builtin_amdgcn_s_sleep(1);
+#if E2SAR_TRACE
+        pass++;
+#endif
     }
+#if E2SAR_TRACE
+    if (__ballot(want)) {
+        TRACE_FIRST(2, 2, trace_now());
+        TRACE_FIRST(2, 3, pass);
+    }
+#endif
     return res;
 }
 
@@ -788,6 +815,8 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
+    TRACE_WAIT();
+    TRACE_AT(2, 0, trace_now());
 
     const uint32_t spc = stride >> 4;
     const uint32_t nch = gn * spc;
@@ -1561,13 +1590,13 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
 // (k = 1) launch, 4 words per workgroup, to host memory.
 extern "C" int e2sar_hip_debug_trace(int k, uint64_t *out, size_t words)
 {
-    if (k < 0 || k > 1 || words > 8192 * 4) return -1;
+    if (k < 0 || k > 2 || words > 8192 * 4) return -1;
     return hipMemcpyFromSymbol(out, HIP_SYMBOL(e2sar_amd::g_trace), words * 8, (size_t)k * 8192 * 4 * 8,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 extern "C" int e2sar_hip_debug_trace_clear(void)
 {
-    static uint64_t zero[2 * 8192 * 4];
+    static uint64_t zero[3 * 8192 * 4];
     return hipMemcpyToSymbol(HIP_SYMBOL(e2sar_amd::g_trace), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -34,7 +34,9 @@ constexpr uint64_t kAccBytesMask = (1ull << kAccFragShift) - 1ull;
 // Per-event counters (Reassembler::AtomicStats, e2sarDPReassembler.hpp:102-122) + allocator
 // state; the per-packet counters live in ReasShard.
 struct ReasCtl {
+    // every creator's returning atomic lands here: alone on its 128-byte line (A/B: +0.7 %)
     unsigned long long arenaTop;
+    uint64_t padA[15];
     unsigned long long eventSuccess;
     unsigned long long enqueueLoss;
     unsigned long long reassemblyLoss;
@@ -47,7 +49,7 @@ struct ReasCtl {
     uint32_t compactUsed;            // slots claimed in the destination table
     uint32_t pad0;
     uint64_t pad[2];
-    uint64_t pad2[21];
+    uint64_t pad2[6];
 };
 static_assert(sizeof(ReasCtl) % 128 == 0, "shards follow the control block on 128-byte lines");
 

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Timeline of one seg_kernel + reas_kernel launch pair (experiment build with -DE2SAR_TRACE=1).
 
-Runs the bench's default batch (128 x 1 MiB events, MTU 1500) a few times, then records
+Runs the bench's default batch (205 x 1 MiB events, MTU 1500) a few times, then records
 per-workgroup s_memrealtime stamps of one more pair and prints where the time goes:
 launch span, dispatch ramp, classification latency, store phase and the tail.
 Usage: E2SAR_HIP_LIB=build/variants/lib_trace.so python tools/trace_reas.py [--mtu M --event-bytes B --batch N]
@@ -27,7 +27,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--mtu", type=int, default=1500)
     ap.add_argument("--event-bytes", type=int, default=1 << 20)
-    ap.add_argument("--batch", type=int, default=128)
+    ap.add_argument("--batch", type=int, default=205)
     ap.add_argument("--out", default="")
     ap.add_argument("--standalone", action="store_true",
                     help="reassemble a batch segmented earlier, after 1.5 GB of other traffic (cold datagrams)")
@@ -86,6 +86,27 @@ def main():
         if name == "reas":
             cl = (t[:, 1].astype(np.int64) - t[:, 0].astype(np.int64)) * 10 / 1000.0
             r["classify_q"] = [float(x) for x in np.quantile(cl, [0.1, 0.5, 0.9, 1.0])]
+            # classification detail (k = 2): header loads back, first CAS back, lookup done, passes
+            d = np.zeros(8192 * 4, np.uint64)
+            assert L.e2sar_hip_debug_trace(2, d.ctypes.data, d.size) == 0
+            d = d.reshape(-1, 4)[: len(t)].astype(np.int64)
+            s0 = t[:, 0].astype(np.int64)
+            okd = (d[:, 0] != 0) & (d[:, 1] != 0) & (d[:, 2] != 0)
+            q = lambda v: [round(float(x), 2) for x in np.quantile(v[okd], [0.1, 0.5, 0.9])]
+            r["detail_us_q10_50_90"] = {
+                "headers": q((d[:, 0] - s0) * 0.01),
+                "first_cas": q((d[:, 1] - d[:, 0]) * 0.01),
+                "rest_of_lookup": q((d[:, 2] - d[:, 1]) * 0.01),
+                "after_lookup": q((t[:, 1].astype(np.int64) - d[:, 2]) * 0.01),
+                "passes": q(d[:, 3].astype(np.float64) * 100.0),
+            }
+            # first-wave blocks only (started within 2 us of the first)
+            fw = okd & (st < st.min() + 2.0)
+            r["first_wave_blocks"] = int(fw.sum())
+            qf = lambda v: [round(float(x), 2) for x in np.quantile(v[fw], [0.1, 0.5, 0.9])]
+            r["first_wave_detail"] = {"headers": qf((d[:, 0] - s0) * 0.01), "first_cas": qf((d[:, 1] - d[:, 0]) * 0.01),
+                                      "rest_of_lookup": qf((d[:, 2] - d[:, 1]) * 0.01),
+                                      "after_lookup": qf((t[:, 1].astype(np.int64) - d[:, 2]) * 0.01)}
         # concurrency profile: running blocks per 2 us bin
         lo, hi = float(st.min()), float(en[ok].max())
         bins = np.arange(lo, hi + 2, 2.0)

@@ -1335,14 +1335,24 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
     while (G > 1 && G * spc > budget) G >>= 1;
     // Balance the launch over whole residency waves: with ceil(n/G) workgroups = 1.5 x
     // what the chip holds at once, the second wave starts late and the last ~15 us run
-    // half-empty (tools/trace_reas.py). Shrink G so the workgroup count is just under a
-    // whole number of waves (205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
-    // reas_kernel 79.0 -> 77.6 us). Never below G/2.
+    // half-empty (tools/trace_reas.py). Pick G so the workgroup count is just under a
+    // whole number of waves -- one wave more (smaller G) or one fewer (larger G) -- if
+    // that keeps G within [3/4, 4/3] of the budget's G: much smaller groups put more
+    // workgroups on each event's table slot and counter (8 MiB events at MTU 9000 lose
+    // 9 % at G 16 -> 10). 205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
+    // reas_kernel 79.0 -> 77.6 us.
     if (env_u32("E2SAR_REAS_BALANCE", 1, 0, 1)) {
         const uint32_t cap = reas_resident_groups<U>();
         if (cap) {
-            const uint32_t waves = cdiv(cdiv(n, G), cap);
-            G = std::max((G + 1) / 2, std::min(G, cdiv(n, waves * cap)));
+            const uint32_t G0 = G, waves = cdiv(cdiv(n, G0), cap);
+            uint32_t best = G0, bestDev = ~0u;
+            for (uint32_t k = (waves > 1 ? waves - 1 : waves); k <= waves; k++) {
+                const uint32_t c = cdiv(n, k * cap);
+                if (c > 64 || 4u * c < 3u * G0 || 3u * c > 4u * G0) continue;
+                const uint32_t dev = c > G0 ? c - G0 : G0 - c;
+                if (dev < bestDev) best = c, bestDev = dev;
+            }
+            G = best;
         }
     }
     G = env_u32("E2SAR_REAS_G", G, 1, 64);             // A/B knob: exact datagrams per workgroup

@@ -12,6 +12,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
@@ -130,6 +131,16 @@ __global__ __launch_bounds__(256) void patk(const uint8_t *__restrict__ pk, uint
     }
 }
 
+__global__ void fill_random(uint64_t *p, uint64_t n)
+{
+    const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n) return;
+    uint64_t z = (i + 1) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = z ^ (z >> 31);
+}
+
 template <int MODE>
 float runpat(const uint8_t *pk, uint8_t *ev, uint32_t npk, int iters)
 {
@@ -176,8 +187,17 @@ int main(int argc, char **argv)
     uint8_t *src, *dst;
     CHECK(hipMalloc(&src, bytes + 64));
     CHECK(hipMalloc(&dst, bytes + 64));
-    CHECK(hipMemset(src, 1, bytes + 64));
-    printf("{\"bytes\": %llu, \"iters\": %d", (unsigned long long)bytes, iters);
+    // source bytes: "one" (0x01, the default), "zero", or "random" (splitmix64 per word):
+    // HBM moves mostly-zero data measurably faster than uniform random bytes
+    const char *fill = argc > 3 ? argv[3] : "one";
+    if (!strcmp(fill, "random")) {
+        fill_random<<<(unsigned)((bytes + 64) / 8 / 256 + 1), 256>>>((uint64_t *)src, (bytes + 64) / 8);
+        CHECK(hipDeviceSynchronize());
+    } else {
+        CHECK(hipMemset(src, strcmp(fill, "zero") ? 1 : 0, bytes + 64));
+    }
+    CHECK(hipMemset(dst, 0, bytes + 64));
+    printf("{\"bytes\": %llu, \"iters\": %d, \"fill\": \"%s\"", (unsigned long long)bytes, iters, fill);
     printf(", \"aligned\": %.1f", run<0>(src, dst, bytes, 0, iters));
     printf(", \"aligned_nt\": %.1f", run<4>(src, dst, bytes, 0, iters));
     printf(", \"ld_mis4\": %.1f", run<1>(src, dst, bytes, 4, iters));

@@ -488,23 +488,26 @@ __device__ __forceinline__ uint64_t shfl_u64(uint64_t v, int src)
     const uint32_t hi = __shfl((uint32_t)(v >> 32), src);
     return ((uint64_t)hi << 32) | lo;
 }
-__device__ __forceinline__ uint64_t shfl_up_u64(uint64_t v, unsigned d)
+// DPP forms of the wave's neighbour moves and its prefix sum: VALU instructions instead of
+// ds_bpermute round trips through the LDS pipe (the classification runs ~30 of those in a
+// dependent chain otherwise, ~1 us at kernel start).  Whole wave active.
+__device__ __forceinline__ uint32_t lane_prev(uint32_t v, uint32_t fill)     // lane i <- lane i-1
 {
-    const uint32_t lo = __shfl_up((uint32_t)v, d);
-    const uint32_t hi = __shfl_up((uint32_t)(v >> 32), d);
-    return ((uint64_t)hi << 32) | lo;
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x138 /* wave_shr:1 */, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint64_t shfl_down_u64(uint64_t v, unsigned d)
+__device__ __forceinline__ uint32_t lane_next(uint32_t v, uint32_t fill)     // lane i <- lane i+1
 {
-    const uint32_t lo = __shfl_down((uint32_t)v, d);
-    const uint32_t hi = __shfl_down((uint32_t)(v >> 32), d);
-    return ((uint64_t)hi << 32) | lo;
+    return (uint32_t)__builtin_amdgcn_update_dpp((int)fill, (int)v, 0x130 /* wave_shl:1 */, 0xf, 0xf, false);
 }
-__device__ __forceinline__ uint64_t wave_sum_u64(uint64_t v)
+__device__ __forceinline__ uint32_t wave_incl_scan(uint32_t v)
 {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += shfl_down_u64(v, o);
-    return v;   // valid in lane 0
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x111 /* row_shr:1 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x112 /* row_shr:2 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x114 /* row_shr:4 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x118 /* row_shr:8 */, 0xf, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x142 /* row_bcast:15 */, 0xa, 0xf, false);
+    v += (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x143 /* row_bcast:31 */, 0xc, 0xf, false);
+    return v;
 }
 
 // Raw header words of one datagram, loaded before the payload loads of the block so the
@@ -569,9 +572,10 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     }
 
     // ---- runs of equal keys ----
-    const uint64_t pev = shfl_up_u64(ev, 1), nev = shfl_down_u64(ev, 1);
-    const uint32_t pd = __shfl_up(d, 1), nd = __shfl_down(d, 1);
-    const int pok = __shfl_up((int)ok, 1), nok = __shfl_down((int)ok, 1);
+    const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(ev >> 32), 0u) << 32) | lane_prev((uint32_t)ev, 0u);
+    const uint64_t nev = ((uint64_t)lane_next((uint32_t)(ev >> 32), 0u) << 32) | lane_next((uint32_t)ev, 0u);
+    const uint32_t pd = lane_prev(d, 0u), nd = lane_next(d, 0u);
+    const uint32_t pok = lane_prev(ok ? 1u : 0u, 0u), nok = lane_next(ok ? 1u : 0u, 0u);
     const bool head = ok && (lane == 0 || !pok || pev != ev || pd != d);
     const bool tail = ok && (lane == 63 || !nok || nev != ev || nd != d);
 
@@ -593,15 +597,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     }
     // segmented sums over the run (inclusive scans, then difference at the head)
     const uint32_t xb = take ? pl : 0u, xc = take ? 1u : 0u;
-    uint32_t ib = xb, ic = xc;
-#pragma unroll
-    for (unsigned s = 1; s < 64; s <<= 1) {
-        const uint32_t yb = __shfl_up(ib, s), yc = __shfl_up(ic, s);
-        if ((unsigned)lane >= s) {
-            ib += yb;
-            ic += yc;
-        }
-    }
+    const uint32_t ib = wave_incl_scan(xb), ic = wave_incl_scan(xc);
     const uint32_t hb = __shfl(ib - xb, myhead), hc = __shfl(ic - xc, myhead);
 
     Classified out;
@@ -629,7 +625,10 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     const uint64_t np = __builtin_popcountll(__ballot(live));
     const uint64_t nbad = __builtin_popcountll(__ballot(bad));
     const uint64_t nder = __builtin_popcountll(__ballot(derr));
-    const uint64_t tb = wave_sum_u64(live ? (uint64_t)len : 0ull);
+    // 64 lengths summed as 16-bit halves (each half-sum fits 32 bits, whatever the lengths)
+    const uint32_t tl = live ? len : 0u;
+    const uint64_t tb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl & 0xFFFFu), 63) +
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl >> 16), 63) << 16);
     if (lane == 0) {
         ReasShard *sh = R.shards + (shard % kShards);
         if (np) atomicAdd(&sh->totalPackets, (unsigned long long)np);

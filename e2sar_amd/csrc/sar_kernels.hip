@@ -448,10 +448,10 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                     } else {
                         advance = true;                                // another event's slot
                     }
-                } else if (A.x == kBusy || A.x == kReady) {
-                    waiting = true;                                    // not published yet
-                } else {
+                } else if (A.x == kDone || A.x == kLost) {
                     advance = true;                                    // DONE / LOST meanwhile
+                } else {
+                    waiting = true;                // not published yet, or a read that overtook the claim
                 }
             } else {
                 advance = true;                                        // DONE / LOST

@@ -344,6 +344,25 @@ def test_reas_small_table_collisions(hip, reas_mode):
         assert len(got) == 48 and st.errorFlags == 0
 
 
+@pytest.mark.parametrize("group", [1, 7, 33, 49, 63])
+def test_reas_group_sizes(hip, group, monkeypatch):
+    # datagrams per reassembly workgroup other than the power of two the chunk budget gives
+    # (the launcher's wave balancing picks e.g. 49 at the bench's 205-event batches): groups
+    # that cut through runs, events and the float chunk split, against the oracle
+    sizes = [70000, 1, 1437, 33333, 100000, 5000, 2873]
+    evs, pk, ln = _events_stream(7, sizes, 1500, seed=101)
+    starts = np.cumsum([0] + [O.num_packets(s, O.max_pld_len(1500)) for s in sizes])[:-1].tolist()
+    rest = [i for i in range(len(ln)) if i not in starts]
+    random.Random(group).shuffle(rest)
+    order = starts + rest              # offset 0 first, the rest shuffled
+    pk, ln = pk[order], ln[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    monkeypatch.setenv("E2SAR_REAS_G", str(group))
+    got, st, _ = _reas_gpu(hip, pk, ln, True, batches=2, mode="fused")
+    _check_reas(got, st, ref, rst)
+    assert len(got) == 7 and st.errorFlags == 0
+
+
 def test_reas_queue_and_arena_limits(hip, reas_mode):
     # arena too small for all events: the overflow is an enqueue loss, never a fault
     evs, pk, ln = _events_stream(6, 100000, 1500, seed=61)

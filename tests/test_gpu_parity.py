@@ -3,6 +3,7 @@
 Bar: bit-exact datagrams and event bytes, equal counters.  Sizes are ones the oracle
 finishes in seconds; full-size batches are checked through round-trip properties.
 """
+import os
 import random
 
 import numpy as np
@@ -511,3 +512,47 @@ def test_relay_resegments_completed_events(hip):
         op, ol = O.segment_event(host[k], 10 + k, 7, (0xFFFE + i) & 0xFFFF, tick, 3, mp, out.stride)
         b = int(d["pktBase"])
         _assert_same_datagrams(got_pk[b:b + len(ol)], got_ln[b:b + len(ol)], op, ol)
+
+
+# ----------------------------------------------------------------------------------
+# seeded random workloads, end to end
+
+
+@pytest.mark.parametrize("seed", range(int(os.environ.get("E2SAR_RANDOM_SEEDS", "8"))))
+def test_random_workload_segment_then_reassemble(hip, seed):
+    # random event sizes (edge sizes included), MTU, LB version, dataIds, 40-bit event
+    # numbers, 64-bit ticks and misaligned event buffers; the GPU's datagrams must equal the
+    # oracle's, then those datagrams -- all events interleaved, offset 0 first per event
+    # (DESIGN.md 5.3), cut into random batches -- reassemble to the oracle's events and
+    # counters in a random launch form
+    rnd = random.Random(1000 + seed)
+    mtu = rnd.choice([80, 104, 576, 1499, 1500, 4000, 9000])
+    ver = rnd.choice([2, 3])
+    cap = 150_000 if mtu >= 1499 else 20_000
+    evs, keys = [], set()
+    while len(evs) < rnd.randint(1, 12):
+        size = rnd.choice([1, 3, 4, 17, 1435, 1436, 1437]) if rnd.random() < 0.3 else rnd.randint(1, cap)
+        e, d = rnd.randint(0, (1 << 40) - 1), rnd.choice([1, 2, 4321])
+        if (e, d) in keys:
+            continue
+        keys.add((e, d))
+        evs.append((_rng_bytes(seed * 100 + len(evs), size), e, d, rnd.randint(0, 65535), rnd.getrandbits(64)))
+    offsets = [rnd.randint(0, 255) for _ in evs]
+    gp, gl, seg = _segment_gpu(hip, evs, mtu, ver, offsets=offsets)
+    op, ol = _segment_oracle(evs, mtu, ver, seg.stride)
+    _assert_same_datagrams(gp, gl, op, ol)
+
+    per = [O.num_packets(len(b), O.max_pld_len(mtu)) for b, *_r in evs]
+    starts = np.cumsum([0] + per)[:-1].tolist()
+    first = set(starts)
+    rest = [i for i in range(len(ol)) if i not in first]
+    rnd.shuffle(rest)
+    order = starts + rest
+    pk, ln = gp[order], gl[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    for b, e, d, *_r in evs:
+        assert ref[(e, d)] == b.tobytes()
+    mode = rnd.choice(["fused", "split", "pipelined"])
+    got, st, _ = _reas_gpu(hip, pk, ln, True, batches=rnd.randint(1, 4), mode=mode)
+    _check_reas(got, st, ref, rst)
+    assert len(got) == len(evs) and st.errorFlags == 0

@@ -1512,7 +1512,19 @@ __global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict
     }
 }
 
-// copy every datagram slot (stride bytes) to its place in the send buffer
+// copy every datagram slot (stride bytes) to its place in the send buffer.  Workgroup
+// (g, s) = blockIdx (g * kPackSplit + s) recomputes the places of datagrams [256g, 256g+256)
+// (header reads that hit in L2) and copies the s-th of kPackSplit slices of their chunks.
+// A/B at 205 x 1 MiB, MTU 1500, spread landing (route = hist + scan + pack, per batch):
+// split 1/2/4/8 -> 97/92/100/116 us with non-temporal datagram loads, which also leave the
+// Infinity Cache to the packed copy that reassembly reads next (reas 108 -> 79 us).
+#ifndef E2SAR_PACK_SPLIT
+#define E2SAR_PACK_SPLIT 2
+#endif
+constexpr uint32_t kPackSplit = E2SAR_PACK_SPLIT;
+#ifndef E2SAR_PACK_POL
+#define E2SAR_PACK_POL 2      // bit 0: non-temporal stores, bit 1: non-temporal loads
+#endif
 __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
                                                             const uint32_t *__restrict__ lens, uint32_t n, int withLB,
                                                             uint32_t world, uint32_t self,
@@ -1522,7 +1534,8 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
 {
     __shared__ uint32_t pos[kBlock];
     __shared__ uint32_t waveCnt[kBlock / 64][kMaxWorld];
-    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t g = blockIdx.x / kPackSplit, sl = blockIdx.x % kPackSplit;
+    const uint32_t p = g * kBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     const uint32_t dest = (p < n) ? route_dest(pkts, stride, lens, p, withLB, world, self) : 0xFFFFFFFFu;
     uint32_t rank = 0;
@@ -1535,36 +1548,43 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
     if (dest != 0xFFFFFFFFu) {
         uint32_t before = 0;
         for (uint32_t w = 0; w < wv; w++) before += waveCnt[w][dest];
-        const uint32_t q = destBase[dest] + blockBase[(uint64_t)blockIdx.x * world + dest] + before + rank;
+        const uint32_t q = destBase[dest] + blockBase[(uint64_t)g * world + dest] + before + rank;
         pos[threadIdx.x] = q;
-        outLens[q] = lens[p];
+        if (sl == 0) outLens[q] = lens[p];
     }
     __syncthreads();
-    const uint32_t p0 = blockIdx.x * kBlock;
+    const uint32_t p0 = g * kBlock;
     const uint32_t np = (n - p0 < kBlock) ? n - p0 : kBlock;
     const uint32_t spc = stride >> 4;
     const uint32_t nch = np * spc;
     const float rspc = 1.0f / (float)spc;
-    // two-phase rounds of 4 chunks per thread: 4 loads in flight before the stores
+    // this workgroup's slice of the chunks, in two-phase rounds of 4 chunks per thread
+    const uint32_t c0 = (uint32_t)((uint64_t)nch * sl / kPackSplit);
+    const uint32_t c1 = (uint32_t)((uint64_t)nch * (sl + 1) / kPackSplit);
     constexpr int UR = 4;
-    for (uint32_t r0 = 0; r0 < nch; r0 += kBlock * UR) {
+    for (uint32_t r0 = c0; r0 < c1; r0 += kBlock * UR) {
         u32x4 x[UR];
         uint32_t kk[UR], cc[UR];
 #pragma unroll
         for (int u = 0; u < UR; u++) {
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
-            const uint32_t ic = (i < nch) ? i : 0u;
+            const uint32_t ic = (i < c1) ? i : c0;
             uint32_t k = (uint32_t)((float)ic * rspc);
             if (k * spc > ic) k--;
             else if ((k + 1u) * spc <= ic) k++;
             kk[u] = k;
             cc[u] = ic - k * spc;
-            x[u] = ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+            x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
+                                         : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
         }
 #pragma unroll
         for (int u = 0; u < UR; u++) {
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
-            if (i < nch) st16(out + (uint64_t)pos[kk[u]] * stride + 16u * cc[u], x[u]);
+            if (i < c1) {
+                uint8_t *o = out + (uint64_t)pos[kk[u]] * stride + 16u * cc[u];
+                if (E2SAR_PACK_POL & 1) st16_nt(o, x[u]);
+                else st16(o, x[u]);
+            }
         }
     }
 }
@@ -1587,7 +1607,7 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
     hipLaunchKernelGGL(route_hist_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
                        self, blockHist);
     hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kBlock), 0, stream, blockHist, nb, world, counts, destBase);
-    hipLaunchKernelGGL(route_pack_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
+    hipLaunchKernelGGL(route_pack_kernel, dim3(nb * kPackSplit), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
                        self, blockHist, destBase, out, outLens);
     return hipGetLastError();
 }

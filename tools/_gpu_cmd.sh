@@ -1,8 +1,6 @@
 set -e
-O=gpurun_out/final_check; mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > $O/pytest_gpu.log 2>&1 || { tail -40 $O/pytest_gpu.log; exit 1; }
-tail -1 $O/pytest_gpu.log
-timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
-tail -1 $O/smoke.log
-timeout -k 10 300 python bench.py > $O/bench.json 2> $O/bench.err || { tail -20 $O/bench.err; exit 1; }
-cat $O/bench.json
+O=gpurun_out/route2; mkdir -p $O
+timeout -k 10 300 python -u -m pytest tests/test_gpu_parity.py tests/test_dist_gloo.py -x -q --timeout 120 --timeout-method thread -k "route or gloo or dist" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -1 $O/pytest.log
+timeout -k 10 200 python bench.py --cpu-seconds 0 --landing spread > $O/spread.json
+python -c "import json;d=json.load(open('$O/spread.json'));print('spread',d['value'],d['roofline']['avg_launch_ms'])"

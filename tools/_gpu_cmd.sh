@@ -1,9 +1,3 @@
 set -e
-O=gpurun_out/cosched; mkdir -p $O
-run() { n=$1; shift; timeout -k 10 200 python bench.py --cpu-seconds 0 "$@" > $O/$n.json 2> $O/$n.err || { tail -5 $O/$n.err; exit 1; }; python -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['config']['verified_roundtrip'],d['roofline']['avg_launch_ms'])"; }
-run base
-run co205 --reas cosched
-run co128 --reas cosched --batch-events 128
-run co103 --reas cosched --batch-events 103
-run co64 --reas cosched --batch-events 64
-run co160 --reas cosched --batch-events 160
+for r in 1 2; do bash tools/ab_variants.sh ab_u_$r "--steps 20" base u3 u5 u6; done
+for r in 1 2; do for v in base u3 u5 u6; do python -c "import json;d=json.load(open('gpurun_out/ab_u_$r/$v.json'));print('$r $v',d['value'],d['roofline']['avg_launch_ms'])"; done; done

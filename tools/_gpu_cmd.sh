@@ -1,7 +1,5 @@
 set -e
-O=gpurun_out/c3g3; mkdir -p $O
-for r in 1 2 3; do for g in 0 24 32 40; do
-  if [ $g = 0 ]; then unset E2SAR_REAS_G; else export E2SAR_REAS_G=$g; fi
-  timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 30 --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 32 > $O/g${g}_$r.json
-  python -c "import json;d=json.load(open('$O/g${g}_$r.json'));print('$r G $g',d['value'],d['roofline']['avg_launch_ms'])"
-done; done
+E2SAR_HIP_LIB=$GRAFT_REPO_ROOT/build/variants/lib_poll.so timeout -k 10 600 python -u -m pytest tests/test_gpu_parity.py -x -q --timeout 120 --timeout-method thread > gpurun_out/poll_pytest.log 2>&1 || { tail -30 gpurun_out/poll_pytest.log; exit 1; }
+tail -1 gpurun_out/poll_pytest.log
+for r in 1 2 3; do bash tools/ab_variants.sh ab_poll_$r "--steps 20" base poll; bash tools/ab_variants.sh ab_poll9_$r "--steps 20 --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 32" base poll; done
+for r in 1 2 3; do for v in base poll; do python -c "import json;d=json.load(open('gpurun_out/ab_poll_$r/$v.json'));e=json.load(open('gpurun_out/ab_poll9_$r/$v.json'));print('$r $v',d['value'],d['roofline']['avg_launch_ms']['reas_kernel'],'| 8M',e['value'],e['roofline']['avg_launch_ms']['reas_kernel'])"; done; done

@@ -26,6 +26,9 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
+#ifndef E2SAR_REAS_POLL_SLEEP
+#define E2SAR_REAS_POLL_SLEEP 1       // s_sleep units (64 clocks) between slot polls
+#endif
 
 // Occupancy cap of the fused reassembly kernel (0 = whatever its registers allow).
 #ifndef E2SAR_REAS_WAVES
@@ -474,7 +477,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             }
         }
-        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(1);
+        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
 #if E2SAR_TRACE
         pass++;
 #endif

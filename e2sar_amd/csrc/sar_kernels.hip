@@ -55,12 +55,13 @@ constexpr int kBlock = 256;
 #define E2SAR_TRACE 0
 #endif
 #if E2SAR_TRACE
-__device__ uint64_t g_trace[3][8192 * 4];
+constexpr uint32_t kTraceBlocks = 16384;
+__device__ uint64_t g_trace[3][kTraceBlocks * 4];
 #define TRACE_AT(k, slot, i) \
-    do { if (threadIdx.x == 0 && blockIdx.x < 8192) g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
+    do { if (threadIdx.x == 0 && blockIdx.x < kTraceBlocks) g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
 // by the first active lane of wave 0 (inside divergent code)
 #define TRACE_FIRST(k, slot, i) \
-    do { if (threadIdx.x < 64 && blockIdx.x < 8192 && \
+    do { if (threadIdx.x < 64 && blockIdx.x < kTraceBlocks && \
              threadIdx.x == (uint32_t)(__builtin_ffsll((long long)__ballot(1)) - 1)) \
              g_trace[k][blockIdx.x * 4 + (slot)] = (i); } while (0)
 #define TRACE_WAIT() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
@@ -1628,13 +1629,13 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
 // (k = 1) launch, 4 words per workgroup, to host memory.
 extern "C" int e2sar_hip_debug_trace(int k, uint64_t *out, size_t words)
 {
-    if (k < 0 || k > 2 || words > 8192 * 4) return -1;
-    return hipMemcpyFromSymbol(out, HIP_SYMBOL(e2sar_amd::g_trace), words * 8, (size_t)k * 8192 * 4 * 8,
+    if (k < 0 || k > 2 || words > e2sar_amd::kTraceBlocks * 4) return -1;
+    return hipMemcpyFromSymbol(out, HIP_SYMBOL(e2sar_amd::g_trace), words * 8, (size_t)k * e2sar_amd::kTraceBlocks * 4 * 8,
                                hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
 }
 extern "C" int e2sar_hip_debug_trace_clear(void)
 {
-    static uint64_t zero[3 * 8192 * 4];
+    static uint64_t zero[3 * e2sar_amd::kTraceBlocks * 4];
     return hipMemcpyToSymbol(HIP_SYMBOL(e2sar_amd::g_trace), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -61,7 +61,7 @@ def main():
     torch.cuda.synchronize()
     out = {}
     for k, name in ((1, "seg"), (0, "reas")):
-        buf = np.zeros(8192 * 4, np.uint64)
+        buf = np.zeros(16384 * 4, np.uint64)
         assert L.e2sar_hip_debug_trace(k, buf.ctypes.data, buf.size) == 0
         t = buf.reshape(-1, 4)
         t = t[t[:, 0] != 0]
@@ -87,7 +87,7 @@ def main():
             cl = (t[:, 1].astype(np.int64) - t[:, 0].astype(np.int64)) * 10 / 1000.0
             r["classify_q"] = [float(x) for x in np.quantile(cl, [0.1, 0.5, 0.9, 1.0])]
             # classification detail (k = 2): header loads back, first CAS back, lookup done, passes
-            d = np.zeros(8192 * 4, np.uint64)
+            d = np.zeros(16384 * 4, np.uint64)
             assert L.e2sar_hip_debug_trace(2, d.ctypes.data, d.size) == 0
             d = d.reshape(-1, 4)[: len(t)].astype(np.int64)
             s0 = t[:, 0].astype(np.int64)

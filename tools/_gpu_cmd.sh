@@ -1,4 +1,3 @@
 set -e
-E2SAR_HIP_LIB=$GRAFT_REPO_ROOT/build/variants/lib_trace.so timeout -k 10 200 python tools/trace_reas.py > gpurun_out/tr_seg.json
-python -c "
-import json;d=json.load(open('gpurun_out/tr_seg.json'))['seg'];print({k:v for k,v in d.items() if k!='running_per_2us'});print(d['running_per_2us'])"
+O=gpurun_out/bsweep; mkdir -p $O
+for r in 1 2; do for b in 180 192 205 216 228; do timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 20 --batch-events $b > $O/b${b}_$r.json; python -c "import json;d=json.load(open('$O/b${b}_$r.json'));print('$r b$b',d['value'],d['roofline']['avg_launch_ms'])"; done; done

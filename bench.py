@@ -53,6 +53,8 @@ def parse():
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
+    ap.add_argument("--table-factor", type=int, default=8,
+                    help="event-table slots = next power of two >= factor x events per step")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args()
 
@@ -191,7 +193,7 @@ def main():
     nbuf = 2 if (args.overlap or args.reas == "pipelined") else 1
     bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
     table = 1
-    while table < 2 * E:
+    while table < args.table_factor * E:
         table <<= 1
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096)

@@ -1,5 +1,4 @@
 set -e
-O=gpurun_out/rehearse4; mkdir -p $O
-export E2SAR_BENCH_BACKEND=gloo E2SAR_BENCH_SHARE_GPU=1
-timeout -k 10 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 --master-addr 127.0.0.1 --master-port 29541 bench.py --gpus 4 --steps 5 --warmup 2 --events 256 > $O/own4.json 2> $O/own4.err || { tail -20 $O/own4.err; exit 1; }
-python -c "import json;d=json.load(open('$O/own4.json'));print(d['n_gpus'],d['value'],d['config']['parallelism'],d['config']['verified_roundtrip'])"
+O=gpurun_out/tbl; mkdir -p $O
+for r in 1 2; do for f in 2 4 8 16; do timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 20 --table-factor $f > $O/f${f}_$r.json; python -c "import json;d=json.load(open('$O/f${f}_$r.json'));print('$r factor $f',d['value'],d['roofline']['avg_launch_ms'])"; done; done
+for f in 2 8; do timeout -k 10 200 python bench.py --cpu-seconds 0 --steps 20 --table-factor $f --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 32 > $O/c3f${f}.json; python -c "import json;d=json.load(open('$O/c3f${f}.json'));print('cfg3 factor $f',d['value'],d['roofline']['avg_launch_ms'])"; done

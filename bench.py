@@ -460,6 +460,7 @@ def main():
                              f"LB v{args.lb_version} + RE headers, withLBHeader, {args.batch_events} events per "
                              f"launch, segment -> reassemble in HBM"),
                 "events_per_rank": E, "event_bytes": B, "mtu": args.mtu, "batch_events": args.batch_events,
+                "table_slots": max(table, 64),
                 "parallelism": (f"eventNum % {world} sharding (no collective)" if args.landing == "own" else
                                 f"eventNum % {world} owners, datagrams land spread: route + all-to-all-v "
                                 f"({backend}) + reassemble"),

@@ -159,6 +159,29 @@ def test_event_numbering_and_overrides(E):
     assert evs[0][:2] == (100, DATA_ID) and evs[1] == (101, 77, 0x1234) and evs[2][:2] == (102, DATA_ID)
 
 
+def test_ticks_as_re_event_num(E):
+    # ticksAsREEventNum: the RE eventNum carries the LB tick (e2sarDPSegmenter.cpp:723-724)
+    port = next_port()
+    t, got = capture(port, 2)
+    f = E.DataPlane.Segmenter.SegmenterFlags()
+    f.useCP = False
+    f.mtu = 1500
+    f.numSendSockets = 1
+    f.ticksAsREEventNum = True
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync=192.168.0.1:12345&data={DP}:{port}",
+                     E.EjfatURI.TokenType.instance)
+    seg = E.DataPlane.Segmenter(uri, DATA_ID, EVENTSRC_ID, f)
+    ok(seg.OpenAndStart())
+    ok(seg.sendEvent(SEND_STR, len(SEND_STR), 5, 0, 0))
+    ok(seg.sendEvent(SEND_STR, len(SEND_STR), 6, 0, 0))
+    t.join()
+    seg.stopThreads()
+    assert len(got) == 2
+    for d in got:
+        tick = int.from_bytes(d[8:16], "big")
+        assert O.re_parse(d[16:36])[4] == tick and tick > (1 << 40)   # a microsecond clock, not 5 / 6
+
+
 def test_segmenter_sanity_checks(E):
     uri = E.EjfatURI(f"ejfat://u@1.2.3.4:1/lb/1?data={DP}:{next_port()}")
     f = E.DataPlane.Segmenter.SegmenterFlags()

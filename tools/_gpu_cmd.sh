@@ -1,9 +1,3 @@
 set -e
-O=gpurun_out/cfg4; mkdir -p $O
-run() { n=$1; shift; timeout -k 10 200 python bench.py --cpu-seconds 0 "$@" > $O/$n.json; python -c "import json;d=json.load(open('$O/$n.json'));print('$n',d['value'],d['config']['verified_roundtrip'],d['roofline']['avg_launch_ms'])"; }
-run mtu1500_1m_lbv3 --lb-version 3
-run mtu9000_1m --mtu 9000
-run mtu9000_8m_b32 --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 32
-run mtu9000_8m_b24 --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 24
-run mtu1500_1m_spread_landing --landing spread
-run mtu1500_1m_perf_payload --payload perf
+O=gpurun_out/perf_tool; mkdir -p $O
+for m in 9000 1500; do timeout -k 10 200 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m $m --rate -1 --port 10600 > $O/m$m.txt 2>&1 || { tail -20 $O/m$m.txt; exit 1; }; tail -6 $O/m$m.txt; done

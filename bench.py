@@ -6,9 +6,18 @@ into LB+RE datagrams (MTU 1500 -> 731 per event) and the datagrams are reassembl
 into a fresh event arena, batch by batch (default 205 events = 149,855 datagrams =
 221 MB of datagram slots per batch, so a batch's datagrams can stay in the 256 MiB
 Infinity Cache between the two kernels; A/B: 128 -> 1295 GiB/s, 192 -> 1331,
-205 -> 1351, 228 -> 1314, 256 -> 1187).  Inputs (event bytes + the 40-byte-per-event descriptor tables) are resident
-in HBM before timing starts.  N>1: one process per GPU (torch.distributed.run), events
-sharded by eventNum % world (weak scaling, no data-path collective).
+205 -> 1351, 228 -> 1314, 256 -> 1187).  Inputs (event bytes + the 40-byte-per-event
+descriptor tables) are resident in HBM before timing starts.
+
+N>1: one process per GPU.  `python bench.py --gpus N` started without WORLD_SIZE starts
+`torch.distributed.run --nproc-per-node N` itself (a child process, before any GPU call)
+and exits with its status; every rank checks WORLD_SIZE == --gpus.  Events are sharded
+by eventNum % world (weak scaling, no data-path collective); `--landing spread` adds the
+route + all-to-all-v exchange of config 4.
+
+A second, separately reported leg (`reas_cold`) times the receive side alone on
+datagrams written long before (every batch in its own buffer, 1.1 GB in all, so each
+launch reads them back from HBM, not from the Infinity Cache): the real receive path.
 
 Prints ONE JSON line on rank 0.
 """
@@ -17,6 +26,8 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -25,9 +36,10 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+METRIC = "GiB/s event payload segmented+reassembled, device-resident, 1/2/4/8 MI355X"
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -39,12 +51,15 @@ def parse():
                     help="events per segment/reassemble launch (205 x 1 MiB: 150K datagrams, 221 MB: five "
                          "launches per 1024-event step whose datagram batch still fits the 256 MiB Infinity Cache)")
     ap.add_argument("--lb-version", type=int, default=2)
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget (0 = skip)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="CPU baseline budget per thread count (0 = skip)")
     ap.add_argument("--payload", choices=["random", "perf"], default="random",
                     help="random: seeded uniform bytes; perf: e2sar_perf's event (head 'This is a start of "
                          "event payload', tail '...the end', bin/e2sar_perf.cpp:27-28,153-154; zeros between)")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
+    ap.add_argument("--graph-steps", type=int, default=0,
+                    help="steps captured in one HIP graph (0: the largest of 4, 2, 1 that divides --steps); "
+                         "the timed region still runs exactly --steps steps")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
     ap.add_argument("--reas", choices=["fused", "split", "pipelined"], default="fused",
                     help="fused: one reassemble_batch launch per batch; split: classify + scatter launches "
@@ -55,8 +70,11 @@ def parse():
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
     ap.add_argument("--table-factor", type=int, default=8,
                     help="event-table slots = next power of two >= factor x events per step")
+    ap.add_argument("--cold-steps", type=int, default=10,
+                    help="steps of the cold receive-only leg (0 = skip): reassembly of datagrams that were "
+                         "written long before and are read back from HBM")
     ap.add_argument("--quiet", action="store_true")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 def log(args, *a):
@@ -64,12 +82,48 @@ def log(args, *a):
         print(*a, file=sys.stderr, flush=True)
 
 
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch_ranks(args) -> int:
+    """`--gpus N` without a launcher: run this script under torch.distributed.run as a child
+    process (nothing here has touched the GPU) and return its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def host_cpu_info() -> dict:
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        allowed = len(os.sched_getaffinity(0))
+    except AttributeError:
+        allowed = os.cpu_count() or 1
+    return {"nproc": os.cpu_count(), "allowed": allowed, "model": model}
+
+
 def cpu_baseline(args, budget_s: float):
     """The oracle (plain-C restatement of _send + recv body) on the host cores, on a bounded
     sample of the same workload: each thread segments + reassembles its own 16 events of
-    event-bytes repeatedly.  Timed on 1 thread and on T threads (the box's CPU share,
-    OMP_NUM_THREADS, at most 16; ctypes releases the GIL around every C call), budget_s
-    each; the T-thread rate is the reported baseline."""
+    event-bytes repeatedly.  Timed on 1 thread and on T threads, budget_s each; the
+    T-thread rate is the reported baseline.  T = the CPUs this process may use, capped at
+    16: the GPU box allots 16 host CPUs per GPU (OMP_NUM_THREADS=16 there) although nproc
+    shows the whole machine.  ctypes releases the GIL around every C call."""
     import threading
 
     import numpy as np
@@ -121,11 +175,9 @@ def cpu_baseline(args, budget_s: float):
         dt = time.perf_counter() - t0
         return sum(out) / dt / 2**30, sum(out) // (n_ev * B), dt
 
-    try:
-        share = len(os.sched_getaffinity(0))
-    except AttributeError:
-        share = os.cpu_count() or 1
-    T = max(1, min(16, int(os.environ.get("OMP_NUM_THREADS", share)), share))
+    info = host_cpu_info()
+    omp = int(os.environ.get("OMP_NUM_THREADS", info["allowed"]))
+    T = max(1, min(16, omp, info["allowed"]))
     v1, p1, d1 = run(1)
     vT, pT, dT = run(T) if T > 1 else (v1, p1, d1)
     what = (f"MTU {args.mtu}: oracle segment_event (header + payload memcpy per datagram) then recv "
@@ -133,11 +185,24 @@ def cpu_baseline(args, budget_s: float):
             f"each thread {n_ev} x {B} B events per pass")
     return {"value": round(vT, 4), "unit": "GiB/s", "cores": T, "kind": "port",
             "sample": f"{pT} passes on {T} threads in {dT:.1f} s; {what}",
+            "host": {**info, "threads_used": T,
+                     "cap": "min(16, OMP_NUM_THREADS, sched_getaffinity): the GPU box's CPU share per GPU"},
             "single_core": {"value": round(v1, 4), "cores": 1, "sample": f"{p1} passes in {d1:.1f} s"}}
+
+
+def graph_steps(args) -> int:
+    if args.graph_steps > 0:
+        if args.steps % args.graph_steps:
+            raise SystemExit("--steps must be a multiple of --graph-steps")
+        return args.graph_steps
+    return next(d for d in (4, 2, 1) if args.steps % d == 0)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+
     import torch
     import torch.distributed as dist
 
@@ -146,6 +211,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench: --gpus {args.gpus} but WORLD_SIZE {world}: launch one rank per GPU")
     # E2SAR_BENCH_BACKEND=gloo + E2SAR_BENCH_SHARE_GPU=1 rehearse the N>1 flow with every
     # rank on GPU 0 (a one-GPU box); the driver's multi-GPU runs use RCCL ("nccl").
     backend = os.environ.get("E2SAR_BENCH_BACKEND", "nccl")
@@ -166,18 +233,25 @@ def main():
     seg = sar.DeviceSegmenter(ctx, mtu=args.mtu, lb_hdr_version=args.lb_version)
     mp, stride = seg.max_pld, seg.stride
     npk = sar.num_packets(B, mp)
+    G = graph_steps(args)
 
     # ---- inputs resident in HBM: event bytes + per-batch descriptor tables ----
-    g = torch.Generator(device=dev)
-    g.manual_seed(0xE25A2 + rank)
     ev_stride = (B + 255) // 256 * 256
-    src = torch.randint(0, 256, (E, ev_stride), dtype=torch.uint8, device=dev, generator=g)
-    if args.payload == "perf":
-        head, tail = b"This is a start of event payload", b"...the end"
-        assert B >= len(head) + len(tail)
-        src.zero_()
-        src[:, :len(head)] = torch.tensor(list(head), dtype=torch.uint8, device=dev)
-        src[:, B - len(tail):B] = torch.tensor(list(tail), dtype=torch.uint8, device=dev)
+
+    def make_src(r):
+        """Rank r's source events (regenerable from its seed by any rank, for verification)."""
+        g = torch.Generator(device=dev)
+        g.manual_seed(0xE25A2 + r)
+        s = torch.randint(0, 256, (E, ev_stride), dtype=torch.uint8, device=dev, generator=g)
+        if args.payload == "perf":
+            head, tail = b"This is a start of event payload", b"...the end"
+            assert B >= len(head) + len(tail)
+            s.zero_()
+            s[:, :len(head)] = torch.tensor(list(head), dtype=torch.uint8, device=dev)
+            s[:, B - len(tail):B] = torch.tensor(list(tail), dtype=torch.uint8, device=dev)
+        return s
+
+    src = make_src(rank)
     if args.landing == "own":
         evnum = lambda i: i * world + rank      # every local event is owned here: eventNum % world == rank
     else:
@@ -188,15 +262,38 @@ def main():
         plans.append(seg.plan([(src[i].data_ptr(), B, evnum(i), 4321, 1 + (evnum(i) * 0x9E37) % 65535,
                                 (1 << 48) + evnum(i)) for i in idx]))
     max_batch_pk = max(p.total_packets for p in plans)
+    step_pk = sum(p.total_packets for p in plans)
     if args.reas == "pipelined" and args.overlap:
         args.overlap = False                    # the pipeline is its own overlap
     nbuf = 2 if (args.overlap or args.reas == "pipelined") else 1
-    bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
     table = 1
     while table < args.table_factor * E:
         table <<= 1
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096)
+
+    spread = args.landing == "spread"
+    if spread:
+        # every batch of the step lands in one buffer (contiguous), so one route and one
+        # all-to-all-v per step move it: one host read of the count matrix per step, which
+        # all_to_all_single needs for its split sizes
+        from e2sar_amd.dist import PacketRouter, exchange as dexchange
+        land = seg.alloc_packets(step_pk)
+        land_off = [0]
+        for p in plans[:-1]:
+            land_off.append(land_off[-1] + p.total_packets)
+        router = PacketRouter(ctx, stride, step_pk, world, rank)
+        recv_cap = 2 * step_pk + 1024
+        recv_bufs = (torch.empty(recv_cap * stride, dtype=torch.uint8, device=dev),
+                     torch.empty(recv_cap, dtype=torch.int32, device=dev))
+        if args.overlap or not args.eager or args.reas != "fused":
+            log(args, "landing=spread: the exchange reads its split sizes on the host -> eager, fused, no overlap")
+        args.overlap = False
+        args.reas = "fused"
+        args.eager = True
+        bufs = []
+    else:
+        bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
     works = [R.alloc_work(max_batch_pk) for _ in range(nbuf)] if args.reas != "fused" else None
     torch.cuda.synchronize()
 
@@ -224,25 +321,29 @@ def main():
             timed("reas_classify_kernel", R.classify, pk, stride, ln, n, w, stream=stream)
             timed("reas_scatter_kernel", R.scatter, pk, stride, n, w, stream=stream)
 
+    def step_spread():
+        """Datagrams land on this rank whatever their owner: route by owner on the GPU, one
+        all-to-all-v over RCCL, reassemble what this rank owns."""
+        lpk, lln = land
+        for p, off in zip(plans, land_off):
+            timed("seg_kernel", seg.segment, p, lpk[off * stride:], lln[off:])
+        spk, sln, cnt = timed("route_kernels", router.route, lpk, lln, step_pk)
+        if world > 1:
+            counts = [int(c) for c in cnt.tolist()]
+            rpk, rln, n = timed("exchange", dexchange, spk, sln, counts, stride, out=recv_bufs)
+        else:
+            rpk, rln, n = spk, sln, step_pk
+        for c0 in range(0, n, max_batch_pk):
+            timed("reas_kernel", R.reassemble, rpk[c0 * stride:], stride, rln[c0:], min(max_batch_pk, n - c0))
+
     def step():
         """One step: recycle the event table/arena, then segment -> reassemble every batch.
         With --overlap, reassembly of batch b runs on a second stream concurrently with
         segmentation of batch b+1 (double-buffered datagram slots)."""
         s0 = torch.cuda.current_stream()
         R.recycle(force=True)
-        if args.landing == "spread":
-            # datagrams land on this rank whatever their owner: route by owner on the GPU,
-            # one all-to-all-v over RCCL, reassemble what this rank owns
-            pk, ln = bufs[0]
-            for p in plans:
-                timed("seg_kernel", seg.segment, p, pk, ln)
-                spk, sln, cnt = timed("route_kernels", router.route, pk, ln, p.total_packets)
-                if world > 1:
-                    rpk, rln, n = timed("exchange", dexchange, spk, sln, [int(c) for c in cnt.tolist()], stride)
-                else:
-                    rpk, rln, n = spk, sln, p.total_packets
-                timed("reas_kernel", R.reassemble, rpk, stride, rln, n)
-            return
+        if spread:
+            return step_spread()
         if args.reas == "pipelined":
             # seg(0), classify(0); then per batch: seg(b+1), [scatter(b) | classify(b+1)]
             # in one launch; buffers b%2 are rewritten by seg(b+2) after that launch.
@@ -285,47 +386,37 @@ def main():
 
     side = torch.cuda.Stream() if args.overlap else None
 
-    router = None
-    if args.landing == "spread":
-        from e2sar_amd.dist import PacketRouter, exchange as dexchange
-        router = PacketRouter(ctx, stride, max_batch_pk, world, rank)
-        if args.overlap or not args.eager or args.reas != "fused":
-            log(args, "landing=spread: counts are read back per batch -> eager, fused, no overlap")
-        args.overlap = False
-        args.reas = "fused"
-        args.eager = True
-
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
 
-    # ---- correctness gate (outside the timed region) ----
+    # ---- correctness gate (outside the timed region): every event byte-exact ----
     def verify_spread():
         recs = R.poll()
         st = R.stats()
         arena = R.arena_tensor()
-        # per-event byte sums of every rank's source events, all-gathered
-        sums = src[:, :B].to(torch.int64).sum(dim=1)
-        ids = torch.tensor([evnum(i) for i in range(E)], dtype=torch.int64, device=dev)
-        table = torch.stack([ids, sums], dim=1)
-        if world > 1:
-            table = table.to(coll_dev)
-            allt = [torch.empty_like(table) for _ in range(world)]
-            dist.all_gather(allt, table)
-            table = torch.cat(allt).to(dev)
-        ref = {int(a): int(b) for a, b in table.tolist()}
-        owned = [e for e in ref if e % world == rank]
-        ok = (len(recs) == len(owned) and st.inProgress == 0 and st.badHeaderDiscards == 0)
+        owned = sum(1 for r in range(world) for i in range(E) if (r * E + i) % world == rank)
+        ok = (len(recs) == owned and st.inProgress == 0 and st.badHeaderDiscards == 0 and st.dataErrCnt == 0
+              and all(r.numFragments == npk for r in recs))
+        by_src = {}
         for r in recs:
+            by_src.setdefault(r.eventNum // E, []).append(r)
+        for s_rank, rs in sorted(by_src.items()):
             if not ok:
                 break
-            ok = int(arena[r.arenaOffset: r.arenaOffset + B].to(torch.int64).sum()) == ref.get(r.eventNum, -1)
+            s = src if s_rank == rank else make_src(s_rank)
+            for r in rs:
+                if not torch.equal(arena[r.arenaOffset: r.arenaOffset + B], s[r.eventNum % E, :B]):
+                    ok = False
+                    break
+            del s
         if not ok:
-            raise SystemExit(f"rank {rank}: spread-landing verification FAILED ({len(recs)} records)")
+            raise SystemExit(f"rank {rank}: spread-landing verification FAILED ({len(recs)} records, "
+                             f"{owned} owned)")
         return True
 
     def verify():
-        if args.landing == "spread":
+        if spread:
             return verify_spread()
         recs = R.poll()
         st = R.stats()
@@ -349,57 +440,73 @@ def main():
         torch.cuda.synchronize()
         verified = verify()
 
-    # ---- the step as one HIP graph (kills per-launch host overhead) ----
-    graph = None
-    if not args.eager:
+    def capture(fn, steps):
+        """`steps` calls of fn as one HIP graph (kills per-launch host overhead)."""
         graph = torch.cuda.CUDAGraph()
         cap = torch.cuda.Stream()
         cap.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(cap):
-            step()                          # warm the capture stream once
+            fn()                            # warm the capture stream once
         torch.cuda.synchronize()
         with torch.cuda.graph(graph, stream=cap):
-            step()
+            for _ in range(steps):
+                fn()
         torch.cuda.synchronize()
         graph.replay()
         torch.cuda.synchronize()
+        return graph
+
+    graph = None
+    if not args.eager:
+        graph = capture(step, G)
         if not args.no_verify:
             verified = verify() and verified is not False
 
+    def run_timed(fn, g, k):
+        """k steps (k/G graph replays, or k eager steps) between barriers; max over ranks."""
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        if g is not None:
+            for _ in range(k // G):
+                g.replay()
+        else:
+            for _ in range(k):
+                fn()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        if world > 1:
+            dist.barrier()
+        el = t1 - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
     # ---- timed region ----
     K = args.steps
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(K):
-        if graph is not None:
-            graph.replay()
-        else:
-            step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=coll_dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = run_timed(step, graph, K)
 
     # ---- per-kernel durations: HIP events around each launch of the step, eager, on the
     # stream the kernels run on (the step is single-stream unless --overlap) ----
+    def kernel_times(fn, steps):
+        timing.clear()
+        timing_on[0] = True
+        for _ in range(max(1, steps)):
+            fn()
+        torch.cuda.synchronize()
+        timing_on[0] = False
+        per = {}
+        for name, e0, e1 in timing:
+            per.setdefault(name, []).append(e0.elapsed_time(e1))
+        return per
+
     was_overlap = args.overlap
     args.overlap = False
-    timing_on[0] = True
-    for _ in range(max(1, args.roofline_steps)):
-        step()
-    torch.cuda.synchronize()
-    timing_on[0] = False
+    per = kernel_times(step, args.roofline_steps)
     args.overlap = was_overlap
-    per = {}
-    for name, e0, e1 in timing:
-        per.setdefault(name, []).append(e0.elapsed_time(e1))
     avg = {k: sum(v) / len(v) for k, v in per.items()}
     per_launch_events = sum(p.n_events for p in plans) / len(plans)
     # algorithmic bytes of one launch of each bandwidth kernel (SURVEY 8(d)):
@@ -411,6 +518,11 @@ def main():
                                           "reas_scatter_classify_kernel")]
     dom = max(bw_kernels, key=lambda k: sum(per[k]))      # most time in the step
     dom_ms = avg[dom]
+    if spread and dom == "reas_kernel":
+        # the spread leg reassembles this rank's owned events in launches of max_batch_pk
+        # datagrams (the last one fewer): average algorithmic bytes per launch
+        owned = sum(1 for r in range(world) for i in range(E) if (r * E + i) % world == rank)
+        launch_bytes = owned * (2 * B + 36 * npk) / (len(per[dom]) / max(1, args.roofline_steps))
     achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
 
     # HBM traffic per launch of the dominant kernel, from the committed rocprofv3 PMC passes
@@ -418,7 +530,7 @@ def main():
     traffic = None
     traffic_src = None
     pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path):
+    if os.path.exists(pmc_path) and not spread:
         try:
             with open(pmc_path) as f:
                 pmc = json.load(f)
@@ -428,7 +540,7 @@ def main():
                 for k, v in pmc["kernels"].items():
                     if k.startswith(dom):
                         traffic = int(v["hbm_bytes_per_launch"])
-                        traffic_src = pmc.get("file", "profiles/round1/final/pmc_summary.json")
+                        traffic_src = pmc.get("file", "profiles/pmc_latest.json")
         except (OSError, ValueError, KeyError):
             traffic = None
 
@@ -436,13 +548,49 @@ def main():
     value = total_payload / elapsed / 2**30
     step_bytes = E * (4 * B + 72 * npk)
 
+    # ---- cold receive-only leg: every batch's datagrams in a buffer of its own, written
+    # once before timing; a step reassembles them all (1.1 GB of datagrams > the 256 MiB
+    # Infinity Cache, so each launch reads its batch back from HBM) ----
+    cold = None
+    if args.cold_steps > 0 and not spread:
+        cbufs = [seg.alloc_packets(p.total_packets) for p in plans]
+        for p, (pk, ln) in zip(plans, cbufs):
+            seg.segment(p, pk, ln)
+        torch.cuda.synchronize()
+
+        def cstep():
+            R.recycle(force=True)
+            for p, (pk, ln) in zip(plans, cbufs):
+                timed("reas_kernel", R.reassemble, pk, stride, ln, p.total_packets)
+
+        cstep()
+        torch.cuda.synchronize()
+        cver = None if args.no_verify else verify()
+        cgraph = None if args.eager else capture(cstep, G)
+        ck = max(G, args.cold_steps // G * G)
+        cel = run_timed(cstep, cgraph, ck)
+        cper = kernel_times(cstep, args.roofline_steps)
+        c_ms = sum(cper["reas_kernel"]) / len(cper["reas_kernel"])
+        c_ach = launch_bytes / (c_ms * 1e-3) / 1e9
+        cold = {
+            "what": "reas_kernel alone on datagrams written long before (one buffer per batch, "
+                    f"{step_pk * stride / 1e9:.2f} GB per step, read back from HBM); value = payload "
+                    "reassembled per second",
+            "value": round(E * B * world * ck / cel / 2**30, 3), "unit": "GiB/s", "steps": ck,
+            "ms_per_step": round(cel / ck * 1e3, 4), "verified": cver,
+            "roofline": {"bound": "hbm", "kernel": "reas_kernel", "achieved": round(c_ach, 1),
+                         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(c_ach / HBM_PEAK_GBS, 4),
+                         "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(launch_bytes)},
+        }
+        del cbufs
+
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         cpu = cpu_baseline(args, args.cpu_seconds)
 
     if rank == 0:
         line = {
-            "metric": "GiB/s event payload segmented+reassembled, device-resident, 1/2/4/8 MI355X",
+            "metric": METRIC,
             "value": round(value, 3),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -461,10 +609,10 @@ def main():
                              f"launch, segment -> reassemble in HBM"),
                 "events_per_rank": E, "event_bytes": B, "mtu": args.mtu, "batch_events": args.batch_events,
                 "table_slots": max(table, 64),
-                "parallelism": (f"eventNum % {world} sharding (no collective)" if args.landing == "own" else
+                "parallelism": (f"eventNum % {world} sharding (no collective)" if not spread else
                                 f"eventNum % {world} owners, datagrams land spread: route + all-to-all-v "
                                 f"({backend}) + reassemble"),
-                "launch": "eager" if args.eager else "hipGraph per step",
+                "launch": "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times",
                 "overlap": bool(args.overlap),
                 "reassembly": {"fused": "reas_kernel per batch",
                                "split": "reas_classify_kernel + reas_scatter_kernel per batch",
@@ -489,6 +637,7 @@ def main():
                 "algorithmic_bytes_per_launch": int(launch_bytes),
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
             },
+            "reas_cold": cold,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)

@@ -24,29 +24,46 @@ def owner(event_num: int, world: int) -> int:
 
 
 def exchange(send_pk: torch.Tensor, send_ln: torch.Tensor, counts: List[int], stride: int,
-             group: Optional[dist.ProcessGroup] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
+             group: Optional[dist.ProcessGroup] = None,
+             out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
     """All-to-all-v of datagram slots.
 
     send_pk: uint8, sum(counts)*stride bytes, the span for rank d at offset
     sum(counts[:d])*stride; send_ln: int32 lengths in the same order; counts: datagrams per
-    destination rank.  Returns (recv_pk, recv_ln, n_recv), spans ordered by source rank.
-    Works on any backend that implements all_to_all_single (nccl/RCCL on GPU, gloo on CPU).
+    destination rank (host ints: all_to_all_single takes its split sizes on the host).
+    out: optional preallocated (recv_pk, recv_ln) used when large enough, so a steady
+    stream of batches does not allocate per call.  Returns (recv_pk, recv_ln, n_recv),
+    spans ordered by source rank.  Backends: nccl (RCCL) on device tensors; gloo, whose
+    all-to-all takes host tensors, through host staging copies (the CPU rehearsal path).
     """
     world = dist.get_world_size(group)
     if len(counts) != world:
         raise ValueError("counts must have one entry per rank")
     dev = send_pk.device
-    cnt = torch.tensor(counts, dtype=torch.int64, device=dev)
+    via_host = dist.get_backend(group) == "gloo" and send_pk.is_cuda
+    cdev = torch.device("cpu") if via_host else dev
+    cnt = torch.tensor(counts, dtype=torch.int64, device=cdev)
     rcnt = torch.empty_like(cnt)
     dist.all_to_all_single(rcnt, cnt, group=group)
     rc = [int(x) for x in rcnt.tolist()]
     n_recv = sum(rc)
-    recv_pk = torch.empty(max(n_recv, 1) * stride, dtype=torch.uint8, device=dev)
-    recv_ln = torch.empty(max(n_recv, 1), dtype=torch.int32, device=dev)
+    if out is not None and out[0].numel() >= n_recv * stride and out[1].numel() >= n_recv and out[0].device == dev:
+        recv_pk, recv_ln = out
+    else:
+        recv_pk = torch.empty(max(n_recv, 1) * stride, dtype=torch.uint8, device=dev)
+        recv_ln = torch.empty(max(n_recv, 1), dtype=torch.int32, device=dev)
     n_send = sum(counts)
-    dist.all_to_all_single(recv_pk[: n_recv * stride], send_pk[: n_send * stride],
-                           [c * stride for c in rc], [c * stride for c in counts], group=group)
-    dist.all_to_all_single(recv_ln[:n_recv], send_ln[:n_send], rc, list(counts), group=group)
+    spk, sln = send_pk[: n_send * stride], send_ln[:n_send]
+    rpk, rln = recv_pk[: n_recv * stride], recv_ln[:n_recv]
+    if via_host:
+        hpk, hln = torch.empty(n_recv * stride, dtype=torch.uint8), torch.empty(n_recv, dtype=torch.int32)
+        dist.all_to_all_single(hpk, spk.cpu(), [c * stride for c in rc], [c * stride for c in counts], group=group)
+        dist.all_to_all_single(hln, sln.cpu(), rc, list(counts), group=group)
+        rpk.copy_(hpk)
+        rln.copy_(hln)
+    else:
+        dist.all_to_all_single(rpk, spk, [c * stride for c in rc], [c * stride for c in counts], group=group)
+        dist.all_to_all_single(rln, sln, rc, list(counts), group=group)
     return recv_pk, recv_ln, n_recv
 
 

@@ -170,10 +170,11 @@ class DeviceReassembler:
 
     def __init__(self, ctx: Context, with_lb_header: bool = False, table_slots: int = 4096,
                  queue_capacity: int = 4096, lost_capacity: int = 4096, arena_bytes: int = 1 << 30,
-                 compactable: bool = False):
+                 compactable: bool = False, flags: int = 0):
         self.ctx = ctx
+        flags |= _capi.REAS_COMPACTABLE if compactable else 0
         cfg = _capi.ReasConfig(1 if with_lb_header else 0, table_slots, queue_capacity,
-                               lost_capacity, arena_bytes, _capi.REAS_COMPACTABLE if compactable else 0, 0)
+                               lost_capacity, arena_bytes, flags, 0)
         h = C.c_void_p()
         check(lib().e2sar_hip_reas_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self._h = h

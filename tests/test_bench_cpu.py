@@ -20,3 +20,34 @@ def test_cpu_baseline_reports_the_contract_fields(monkeypatch):
     assert r["unit"] == "GiB/s" and r["kind"] == "port" and r["value"] > 0
     assert 1 <= r["cores"] <= 2 and r["single_core"]["cores"] == 1 and r["single_core"]["value"] > 0
     assert "MTU 1500" in r["sample"]
+
+
+def test_gpus_n_starts_one_rank_per_gpu(monkeypatch):
+    # `python bench.py --gpus 2` with no launcher: bench starts torch.distributed.run with
+    # 2 ranks as a child process and exits with its status (nothing touches the GPU first)
+    calls = []
+    monkeypatch.setattr(sys, "argv", ["bench.py", "--gpus", "2", "--steps", "4"])
+    monkeypatch.delenv("WORLD_SIZE", raising=False)
+    monkeypatch.setattr(bench.subprocess, "call", lambda cmd, env=None: calls.append((cmd, env)) or 7)
+    try:
+        bench.main()
+    except SystemExit as e:
+        assert e.code == 7
+    else:
+        raise AssertionError("bench.main() did not exit with the launcher's status")
+    (cmd, env), = calls
+    assert cmd[1:3] == ["-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and "--master-addr=127.0.0.1" in cmd
+    assert cmd[-4:] == [bench.os.path.abspath(bench.__file__), "--gpus", "2", "--steps", "4"][-4:]
+    assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_graph_steps_divides_the_timed_steps():
+    for steps, g in ((20, 4), (10, 2), (7, 1), (5, 1)):
+        assert bench.graph_steps(bench.parse(["--steps", str(steps)])) == g
+    assert bench.graph_steps(bench.parse(["--steps", "6", "--graph-steps", "3"])) == 3
+
+
+def test_cpu_info_fields():
+    info = bench.host_cpu_info()
+    assert info["nproc"] >= 1 and 1 <= info["allowed"] <= info["nproc"]

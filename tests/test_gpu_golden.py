@@ -1,0 +1,150 @@
+"""The committed fixtures (tests/golden/sar_golden.json) through the HIP path.
+
+Segmentation: every datagram of the full-byte cases, and for the large seeded events the
+committed datagram count, first/last headers, last length and SHA-256 of the datagram
+stream, compared with the committed values directly (not with a live oracle).
+Reassembly: all seven reference-behaviour cases (in order, interleaved, late offset 0,
+duplicate fragment, bad version, no LB header, queue full) through reas_kernel in every
+launch form, one datagram per launch (arrival order, as the reference's receive thread
+sees it) and the whole case as one batch.
+"""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+import sar_inputs as S
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "sar_golden.json")
+STATS = ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt", "enqueueLoss",
+         "reassemblyLoss", "inProgress")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    with open(GOLDEN) as f:
+        return json.load(f)
+
+
+def _segment(ctx, payloads, mtu, ver, metas):
+    """payloads: list of np.uint8; metas: (eventNum, dataId, entropy, lbTick)."""
+    import torch
+    from e2sar_amd import sar
+    seg = sar.DeviceSegmenter(ctx, mtu=mtu, lb_hdr_version=ver)
+    offs, cur = [], 0
+    for p in payloads:
+        cur = (cur + 255) // 256 * 256
+        offs.append(cur)
+        cur += len(p)
+    host = np.zeros(max(cur, 1), np.uint8)
+    for p, o in zip(payloads, offs):
+        host[o:o + len(p)] = p
+    d = torch.from_numpy(host).to(ctx.torch_device)
+    plan = seg.plan([(d.data_ptr() + o, len(p), *m) for p, o, m in zip(payloads, offs, metas)])
+    pk, ln = seg.alloc_packets(plan.total_packets)
+    seg.segment(plan, pk, ln)
+    torch.cuda.synchronize()
+    n = plan.total_packets
+    return pk[: n * seg.stride].view(n, seg.stride).cpu().numpy(), ln[:n].cpu().numpy().astype(np.uint32), plan
+
+
+def test_golden_segment_full_datagrams(hip, golden):
+    for c in golden["segment_full"]:
+        payload = np.frombuffer(bytes.fromhex(c["payload_hex"]), np.uint8)
+        gp, gl, _ = _segment(hip, [payload], c["mtu"], c["lbHdrVersion"],
+                             [(c["eventNum"], c["dataId"], c["entropy"], c["lbTick"])])
+        got = [gp[k, : int(gl[k])].tobytes().hex() for k in range(len(gl))]
+        assert got == c["datagrams_hex"], c["name"]
+
+
+def test_golden_segment_digests(hip, golden):
+    for c in golden["segment"]:
+        evs = c["events"]
+        payloads = [S.event_bytes(e["eventNum"], c["bytes"]) for e in evs]
+        for e, p in zip(evs, payloads):
+            assert hashlib.sha256(p.tobytes()).hexdigest() == e["event_sha256"]
+        gp, gl, plan = _segment(hip, payloads, c["mtu"], c["lbHdrVersion"],
+                                [(e["eventNum"], e["dataId"], e["entropy"], e["lbTick"]) for e in evs])
+        base = 0
+        for e in evs:
+            n = e["numPackets"]
+            p, l = gp[base:base + n], gl[base:base + n]
+            assert p[0, :36].tobytes().hex() == e["first_hdr"], c["name"]
+            if e.get("second_hdr"):
+                assert p[1, :36].tobytes().hex() == e["second_hdr"], c["name"]
+            assert p[-1, :36].tobytes().hex() == e["last_hdr"], c["name"]
+            assert int(l[-1]) == e["last_len"], c["name"]
+            h = hashlib.sha256()
+            for k in range(n):
+                h.update(p[k, : int(l[k])].tobytes())
+            assert h.hexdigest() == e["datagrams_sha256"], c["name"]
+            base += n
+        assert base == plan.total_packets
+
+
+def _reas_case(ctx, case, mode, per_datagram, flags=0):
+    """Run one reassembly fixture; returns (events {(ev, d): hex}, stats dict, lost records)."""
+    import torch
+    from e2sar_amd import sar
+    dg = [bytes.fromhex(h) for h in case["datagrams_hex"]]
+    stride = max(64, (max(len(d) for d in dg) + 15) // 16 * 16)
+    host = np.zeros((len(dg), stride), np.uint8)
+    lens = np.zeros(len(dg), np.uint32)
+    for k, d in enumerate(dg):
+        host[k, :len(d)] = np.frombuffer(d, np.uint8)
+        lens[k] = len(d)
+    dpk = torch.from_numpy(host.reshape(-1)).to(ctx.torch_device)
+    dln = torch.from_numpy(lens.view(np.int32)).to(ctx.torch_device)
+    qcap = 2 if case["name"].endswith("queue_full_lb") else 1000
+    R = sar.DeviceReassembler(ctx, with_lb_header=case["withLBHeader"], table_slots=64, queue_capacity=qcap,
+                              lost_capacity=64, arena_bytes=1 << 16, flags=flags)
+    spans = [(k, k + 1) for k in range(len(dg))] if per_datagram else [(0, len(dg))]
+    works = [R.alloc_work(len(dg)) for _ in range(2)]
+    for j, (a, b) in enumerate(spans):
+        if mode == "fused":
+            R.reassemble(dpk[a * stride:], stride, dln[a:], b - a)
+        else:
+            R.classify(dpk[a * stride:], stride, dln[a:], b - a, works[j % 2])
+            R.scatter(dpk[a * stride:], stride, b - a, works[j % 2])
+    torch.cuda.synchronize()
+    got = {}
+    for rec in R.poll():
+        got[(rec.eventNum, rec.dataId)] = R.event_bytes(rec).hex()
+    st = R.stats()
+    return got, {k: int(getattr(st, k)) for k in STATS}, R.lost_poll()
+
+
+def _expected(case):
+    return {(e["eventNum"], e["dataId"]): e["hex"] for e in case["events"]}
+
+
+@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("per_datagram", [True, False])
+def test_golden_reassembly_cases(hip, golden, mode, per_datagram):
+    for case in golden["reassemble"]:
+        name = case["name"]
+        got, st, lost = _reas_case(hip, case, mode, per_datagram)
+        exp = case["stats"]
+        if name == "mtu80_late_offset0_quirk_lb":
+            # documented divergence of the default (order-insensitive) path, DESIGN.md 5.3:
+            # the reference replaces the in-progress item when offset 0 arrives late
+            # (e2sarDPReassembler.cpp:361-369), so its event never completes; here every
+            # fragment joins its event.  REAS_REFERENCE_ORDER reproduces the reference
+            # (test_golden_reassembly_reference_order).
+            assert exp["eventSuccess"] == 0 and exp["inProgress"] == 1
+            assert st["eventSuccess"] == 1 and st["inProgress"] == 0
+            assert st["totalPackets"] == exp["totalPackets"] and st["totalBytes"] == exp["totalBytes"]
+            continue
+        if name.endswith("queue_full_lb") and not per_datagram:
+            # three events complete in one launch: which two fit the 2-record queue is the
+            # device's completion order; counts and bytes still match
+            assert st == exp, name
+            assert len(got) == 2 and all(got[k] == h for k, h in _expected(case).items() if k in got)
+            assert len(lost) == 1 and lost[0].enqueueLoss == 1
+            continue
+        assert got == _expected(case), name
+        assert st == exp, (name, st, exp)

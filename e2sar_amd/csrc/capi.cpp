@@ -54,12 +54,42 @@ struct e2sar_hip_reas {
     ReasDev alt{};                   // second slots + arena (COMPACTABLE), same ctl/lists
     void *stateMem = nullptr;        // slots | ctl | shards | completed | lost
     void *altSlots = nullptr;
+    // reference-order mode: sort keys / records / rocPRIM storage, and the PktInfo/FinishRec
+    // work buffer of reassemble_batch (both grow on demand)
+    void *roScratch = nullptr;
+    size_t roScratchBytes = 0;
+    void *roWork = nullptr;
+    size_t roWorkBytes = 0;
     std::mutex mu;
 };
+
+static bool ref_order(const e2sar_hip_reas *r) { return (r->cfg.flags & E2SAR_HIP_REAS_REFERENCE_ORDER) != 0; }
+
+// Grow a device buffer to at least `need` bytes (a quarter more, to amortise).  Waits for
+// the device first: kernels of earlier batches may still read the old buffer.
+static hipError_t grow(void *&buf, size_t &have, size_t need)
+{
+    if (need <= have) return hipSuccess;
+    hipError_t e = hipDeviceSynchronize();
+    if (e != hipSuccess) return e;
+    if (buf) (void)hipFree(buf);
+    buf = nullptr;
+    have = 0;
+    const size_t want = need + need / 4;
+    e = hipMalloc(&buf, want);
+    if (e != hipSuccess) {
+        buf = nullptr;
+        return e;
+    }
+    have = want;
+    return hipSuccess;
+}
 
 // Free whatever a partly built reassembler holds (every pointer starts null).
 static void reas_release(e2sar_hip_reas *r)
 {
+    if (r->roScratch) (void)hipFree(r->roScratch);
+    if (r->roWork) (void)hipFree(r->roWork);
     if (r->altSlots) (void)hipFree(r->altSlots);
     if (r->alt.arena && r->alt.arena != r->dev.arena) (void)hipFree(r->alt.arena);
     if (r->dev.arena) (void)hipFree(r->dev.arena);
@@ -375,10 +405,25 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     }
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
+    if (r->roScratch) (void)hipFree(r->roScratch);
+    if (r->roWork) (void)hipFree(r->roWork);
     delete r;
 }
 
 uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r) { return r ? r->dev.arena : nullptr; }
+
+}  // extern "C"
+
+// Scratch of the reference-order classification for n datagrams (caller holds r->mu).
+static int ro_prepare(e2sar_hip_reas *r, uint32_t n)
+{
+    const size_t need = ro_scratch_bytes(n, r->dev.tableSlots);
+    if (need == 0) return fail(E2SAR_HIP_ERR_SYSTEM, "rocPRIM sort storage query failed");
+    HIP_TRY(grow(r->roScratch, r->roScratchBytes, need));
+    return E2SAR_HIP_OK;
+}
+
+extern "C" {
 
 int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms, void *stream)
@@ -393,6 +438,16 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    if (ref_order(r)) {
+        // classify in arrival order into the internal work buffer, then the scatter kernel
+        if (int rc = ro_prepare(r, nPackets)) return rc;
+        HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
+        hipError_t e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork,
+                                          r->roScratch, r->roScratchBytes, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s);
+        if (e != hipSuccess) return hip_fail(e, "reference-order reassembly launch");
+        return E2SAR_HIP_OK;
+    }
     hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;
@@ -438,7 +493,14 @@ int e2sar_hip_reas_classify(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, s);
+    hipError_t e;
+    if (ref_order(r)) {
+        if (int rc = ro_prepare(r, nPackets)) return rc;
+        e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, r->roScratch,
+                               r->roScratchBytes, s);
+    } else {
+        e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, s);
+    }
     if (e != hipSuccess) return hip_fail(e, "classify launch");
     return E2SAR_HIP_OK;
 }
@@ -483,8 +545,19 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const ui
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    hipError_t e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms,
-                                                d_cwork, s);
+    hipError_t e;
+    if (ref_order(r)) {
+        // arrival order needs the classification of b+1 after that of b, not inside the
+        // scatter of b: two launches, same results
+        e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s);
+        if (e == hipSuccess && cn) {
+            if (int rc = ro_prepare(r, cn)) return rc;
+            e = launch_ro_classify(r->dev, d_cpk, stride, d_clens, cn, now_ms, d_cwork, r->roScratch,
+                                   r->roScratchBytes, s);
+        }
+    } else {
+        e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms, d_cwork, s);
+    }
     if (e != hipSuccess) return hip_fail(e, "scatter_classify launch");
     return E2SAR_HIP_OK;
 }
@@ -500,10 +573,16 @@ int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, v
     return E2SAR_HIP_OK;
 }
 
+// Snapshot of the control block.  Launches may run on any stream (reassemble_batch and the
+// split forms take the caller's stream), so the snapshot waits for the whole device, not
+// just the context stream: every kernel launched through this reassembler before the call
+// has finished, and r->mu (held by the caller) keeps new ones from starting, so the
+// read-modify-write of the list counts in poll / lost_poll cannot race a kernel's
+// completion atomics.
 static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
 {
     HIP_TRY(hipSetDevice(r->ctx->device));
-    HIP_TRY(hipStreamSynchronize(r->ctx->stream));
+    HIP_TRY(hipDeviceSynchronize());
     HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
     if (sum) {
         std::vector<ReasShard> sh(kShards);
@@ -519,6 +598,24 @@ static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
     return E2SAR_HIP_OK;
 }
 
+}  // extern "C"
+
+// Keep records [n, avail) queued by moving them to the front.  hipMemcpy does not allow
+// overlapping ranges, so the move goes in chunks of at most n records (each chunk's
+// source starts n records above its destination: they never overlap).
+template <typename Rec>
+static int slide_down(Rec *base, uint32_t n, uint32_t avail)
+{
+    if (n == 0 || n >= avail) return E2SAR_HIP_OK;
+    for (uint32_t d = 0; d < avail - n; d += n) {
+        const uint32_t k = std::min(n, avail - n - d);
+        HIP_TRY(hipMemcpy(base + d, base + d + n, sizeof(Rec) * k, hipMemcpyDeviceToDevice));
+    }
+    return E2SAR_HIP_OK;
+}
+
+extern "C" {
+
 int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t cap, uint32_t *nOut)
 {
     if (!r || !nOut || (!out && cap)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
@@ -529,11 +626,7 @@ int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t ca
     const uint32_t avail = std::min(c.nCompleted, r->dev.queueCapacity);
     const uint32_t n = std::min(avail, cap);
     if (n) HIP_TRY(hipMemcpy(out, r->dev.completed, sizeof(e2sar_hip_event_rec) * n, hipMemcpyDeviceToHost));
-    if (n < avail) {
-        // keep the tail queued: slide it to the front
-        HIP_TRY(hipMemcpy(r->dev.completed, r->dev.completed + n, sizeof(e2sar_hip_event_rec) * (avail - n),
-                          hipMemcpyDeviceToDevice));
-    }
+    if (int rc2 = slide_down(r->dev.completed, n, avail)) return rc2;
     const uint32_t left = avail - n;
     HIP_TRY(hipMemcpy(&r->dev.ctl->nCompleted, &left, sizeof(uint32_t), hipMemcpyHostToDevice));
     *nOut = n;
@@ -550,9 +643,7 @@ int e2sar_hip_reas_lost_poll(e2sar_hip_reas *r, e2sar_hip_lost_rec *out, uint32_
     const uint32_t avail = std::min(c.nLost, r->dev.lostCapacity);
     const uint32_t n = std::min(avail, cap);
     if (n) HIP_TRY(hipMemcpy(out, r->dev.lost, sizeof(e2sar_hip_lost_rec) * n, hipMemcpyDeviceToHost));
-    if (n < avail)
-        HIP_TRY(hipMemcpy(r->dev.lost, r->dev.lost + n, sizeof(e2sar_hip_lost_rec) * (avail - n),
-                          hipMemcpyDeviceToDevice));
+    if (int rc2 = slide_down(r->dev.lost, n, avail)) return rc2;
     const uint32_t left = avail - n;
     HIP_TRY(hipMemcpy(&r->dev.ctl->nLost, &left, sizeof(uint32_t), hipMemcpyHostToDevice));
     *nOut = n;
@@ -626,13 +717,15 @@ int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    // event counters live between arenaTop and inProgress; list counts after it
+    // the event counters (eventSuccess .. reassemblyLoss), the per-packet shards and the
+    // error flags; the completed / lost records not yet polled stay queued (resetting
+    // statistics in the reference discards no queued event), and so does inProgress, which
+    // counts live table entries, not history
     auto *ctl = reinterpret_cast<uint8_t *>(r->dev.ctl);
-    // kernels, not memset nodes: this call may be captured into a HIP graph
+    // kernels, not memset nodes: this call may be captured into a HIP graph (DESIGN.md 4.4)
     HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, eventSuccess),
                               (offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, eventSuccess)) / 4, s));
     HIP_TRY(launch_zero_words(r->dev.shards, sizeof(ReasShard) * kShards / 4, s));
-    HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, nCompleted), 2, s));
     HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, errorFlags), 1, s));
     return E2SAR_HIP_OK;
 }

@@ -1,0 +1,23 @@
+// ro_sort.hip -- the key sort of the reference-order reassembly mode (rocPRIM radix sort),
+// in a translation unit of its own so the rocPRIM templates do not slow the main build.
+#include <cstring>
+#include <rocprim/device/device_radix_sort.hpp>
+
+#include "sar_kernels.hpp"
+
+namespace e2sar_amd {
+
+hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long *in, unsigned long long *out,
+                        uint32_t n, unsigned endBit, hipStream_t stream)
+{
+    return rocprim::radix_sort_keys(temp, tempBytes, in, out, (size_t)n, 0u, endBit, stream);
+}
+
+size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots)
+{
+    size_t tb = 0;
+    if (ro_sort_keys(nullptr, tb, nullptr, nullptr, n, ro_sort_end_bit(tableSlots), nullptr) != hipSuccess) return 0;
+    return 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(tb);
+}
+
+}  // namespace e2sar_amd

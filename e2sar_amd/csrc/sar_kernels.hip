@@ -264,10 +264,17 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
         rare[u] = false;
         const uint8_t *a = safe;
         if (j < nch) {
-            // k = j / spc via a float reciprocal and a +-1 correction (exact for j < 2^32)
-            uint32_t k = (uint32_t)((float)j * rspc);
-            if (k * spc > j) k--;
-            else if ((k + 1u) * spc <= j) k++;
+            // k = j / spc: a float reciprocal and a +-1 correction while k < 2^22 (the
+            // estimate is then off by less than one); integer division for the datagrams of
+            // larger events (npk is event-uniform, so the branch never diverges)
+            uint32_t k;
+            if (npk < (1u << 22)) {
+                k = (uint32_t)((float)j * rspc);
+                if (k * spc > j) k--;
+                else if ((k + 1u) * spc <= j) k++;
+            } else {
+                k = j / spc;
+            }
             const uint32_t c = j - k * spc;
             const uint32_t off = k * maxPld;
             const uint32_t L = (bytes - off > maxPld) ? maxPld : bytes - off;
@@ -397,10 +404,17 @@ constexpr uint32_t kNoSlot = 0xFFFFFFFFu;
 constexpr uint64_t kNoBuf = ~0ull;
 constexpr uint32_t kSpinLimit = 1u << 22;
 
+// Record B's bvalid in reference-order mode for a key registered by ro_key_kernel whose
+// event item (buffer, counters) does not exist yet: ro_walk_kernel creates items.
+constexpr uint32_t kBNoItem = 2u;
+
 // Called by a whole wave: lanes with want == false only take part in the loop.  The wave
 // loops until every wanting lane has a result, and every pass is straight-line (claim;
 // creators publish; the others read), so a lane never waits inside a divergent branch
 // for a slot that another lane of the same wave is still creating.
+// keyOnly (reference-order mode): a creator registers the key without an event buffer
+// (record B = {kNoBuf, 0, kBNoItem}); the walk that follows creates the items.
+template <bool keyOnly = false>
 __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
                                        uint64_t now)
 {
@@ -427,7 +441,13 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 TRACE_FIRST(2, 1, trace_now());
             }
 #endif
-            if (old == kEmpty) {
+            if (old == kEmpty && keyOnly) {
+                st16_agent(&sl->bufOff, u32x4{(uint32_t)kNoBuf, (uint32_t)(kNoBuf >> 32), 0u, kBNoItem});
+                st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
+                atomicAdd(&R.ctl->tableUsed, 1u);
+                res.slot = h;
+                active = false;
+            } else if (old == kEmpty) {
                 // this lane owns the slot: buffer, then records B and A
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
                 uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
@@ -539,6 +559,56 @@ __device__ __forceinline__ RawHdr load_hdr(const ReasDev &R, const uint8_t *__re
     return h;
 }
 
+// Per-packet counters of one wave (cpp:331-357): one atomic per wave per counter, sharded.
+// Whole wave active.
+__device__ __forceinline__ void wave_stats(const ReasDev &R, bool live, uint32_t len, bool bad, bool derr,
+                                           uint32_t shard)
+{
+    const uint64_t np = __builtin_popcountll(__ballot(live));
+    const uint64_t nbad = __builtin_popcountll(__ballot(bad));
+    const uint64_t nder = __builtin_popcountll(__ballot(derr));
+    // 64 lengths summed as 16-bit halves (each half-sum fits 32 bits, whatever the lengths)
+    const uint32_t tl = live ? len : 0u;
+    const uint64_t tb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl & 0xFFFFu), 63) +
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl >> 16), 63) << 16);
+    if ((threadIdx.x & 63u) == 0) {
+        ReasShard *sh = R.shards + (shard % kShards);
+        if (np) atomicAdd(&sh->totalPackets, (unsigned long long)np);
+        if (tb) atomicAdd(&sh->totalBytes, (unsigned long long)tb);
+        if (nbad) atomicAdd(&sh->badHeaderDiscards, (unsigned long long)nbad);
+        if (nder) atomicAdd(&sh->dataErrCnt, (unsigned long long)nder);
+    }
+}
+
+// RE header of one datagram -> key, offset, event length, payload length (cpp:340-357;
+// REHdr::validate, e2sarHeaders.hpp:98-101).  Datagrams too short for the headers are bad
+// headers; one longer than its slot (a truncated receive) is a data error.
+struct ParsedHdr {
+    uint64_t ev;
+    uint32_t d, off, blen, pl;
+    bool ok, bad, derr;
+};
+__device__ __forceinline__ ParsedHdr parse_hdr(const RawHdr &raw, uint32_t hl, uint32_t stride, bool live)
+{
+    ParsedHdr h{0, 0, 0, 0, 0, false, false, false};
+    if (!live) return h;
+    if (raw.len < hl) {
+        h.bad = true;
+    } else if (raw.len > stride) {
+        h.derr = true;
+    } else if (!re_valid(raw.re.x)) {
+        h.bad = true;
+    } else {
+        h.d = bswap16(raw.re.x >> 16);
+        h.off = bswap32(raw.re.y);
+        h.blen = bswap32(raw.re.z);
+        h.ev = ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4);
+        h.pl = raw.len - hl;
+        h.ok = true;
+    }
+    return h;
+}
+
 // Per-lane classification result; the run tail's counter update is issued during
 // classification and its return value consumed only after the payload stores.
 struct Classified {
@@ -631,31 +701,19 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     out.info.hl = hl;
     if (ok && slot == kNoSlot) derr = true;                    // table full / probe timeout
 
-    // ---- stats: one atomic per wave per counter, sharded ----
-    const uint64_t np = __builtin_popcountll(__ballot(live));
-    const uint64_t nbad = __builtin_popcountll(__ballot(bad));
-    const uint64_t nder = __builtin_popcountll(__ballot(derr));
-    // 64 lengths summed as 16-bit halves (each half-sum fits 32 bits, whatever the lengths)
-    const uint32_t tl = live ? len : 0u;
-    const uint64_t tb = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl & 0xFFFFu), 63) +
-                        ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl >> 16), 63) << 16);
-    if (lane == 0) {
-        ReasShard *sh = R.shards + (shard % kShards);
-        if (np) atomicAdd(&sh->totalPackets, (unsigned long long)np);
-        if (tb) atomicAdd(&sh->totalBytes, (unsigned long long)tb);
-        if (nbad) atomicAdd(&sh->badHeaderDiscards, (unsigned long long)nbad);
-        if (nder) atomicAdd(&sh->dataErrCnt, (unsigned long long)nder);
-    }
+    wave_stats(R, live, len, bad, derr, shard);
     return out;
 }
 
 // Completion (cpp:403-427): erase from the table, count, and hand the event to the
 // completed queue (or record it lost when the queue is full or it had no buffer).
+// keepSlot (reference-order mode): the walk that found the completion already left the
+// slot in its final state (a later fragment of the key may have started a new item).
 __device__ void complete_event(const ReasDev &R, uint32_t slot, uint64_t ev, uint64_t boff, uint32_t bytes,
-                               uint32_t d, uint32_t frags)
+                               uint32_t d, uint32_t frags, bool keepSlot = false)
 {
     ReasSlot *sl = R.slots + slot;
-    st_agent(&sl->state, (uint32_t)kDone);                     // erase from the map (cpp:409)
+    if (!keepSlot) st_agent(&sl->state, (uint32_t)kDone);      // erase from the map (cpp:409)
     atomicAdd(&R.ctl->eventSuccess, 1ull);                     // cpp:426
     atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
     bool lostOnEnqueue = (boff == kNoBuf);
@@ -939,6 +997,7 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(Reas
 // own stores (the bytes of every workgroup are visible at the end of that launch).
 
 constexpr uint32_t kPktCompletes = 0x80000000u;
+constexpr uint32_t kFinKeepSlot = 0x80000000u;     // FinishRec.slot flag (reference-order mode)
 
 // One wave: classify datagrams [p0, p0+64) of the batch.
 __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const uint8_t *__restrict__ pkts,
@@ -1030,7 +1089,8 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
 
     if (fins) {
         const FinishRec f = fin[g0 + lane];
-        if (f.slot < R.tableSlots) complete_event(R, f.slot, f.ev, f.boff, f.bytes, f.d, f.frags);
+        const uint32_t fs = f.slot & ~kFinKeepSlot;
+        if (fs < R.tableSlots) complete_event(R, fs, f.ev, f.boff, f.bytes, f.d, f.frags, (f.slot & kFinKeepSlot) != 0u);
         else atomicOr(&R.ctl->errorFlags, 8u);
     }
 }
@@ -1070,6 +1130,158 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
         return;
     }
     scatter_group<U>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+}
+
+// ---------------------------------------------------------------------------------
+// reassembly in the reference's arrival order (E2SAR_HIP_REAS_REFERENCE_ORDER)
+//
+// The reference's receive body takes datagrams one at a time (e2sarDPReassembler.cpp:
+// 335-427), and for some inputs the order decides the outcome: a fragment with
+// bufferOffset 0 always starts a new item, replacing (dropping) an item in progress under
+// the same key (cpp:361-369); a fragment whose key has no item starts one (cpp:376-384),
+// also after its event completed; completion is tested after every fragment (cpp:403), so
+// a duplicate that arrives before the last fragment makes curBytes overshoot while one that
+// arrives after completion starts an item of its own.  This mode reproduces that for any
+// arrival order (batch order, then datagram order within a batch):
+//   ro_key_kernel  : parse and validate every datagram (counters as classify_wave), register
+//                    its key in the table (find_or_create<keyOnly>) and emit a sort key
+//                    slot << 32 | position and a 16-byte record {off, plen, blen, hl};
+//   ro_sort_keys   : rocPRIM radix sort of the keys (ro_sort.hip);
+//   ro_walk_kernel : one thread per key walks that key's datagrams in arrival order with the
+//                    reference's rules, creating items (arena buffers) as it goes, and writes
+//                    the PktInfo / FinishRec work records of the split form;
+//   reas_scatter_kernel then moves the bytes and publishes the completions.
+
+// sort key of a datagram that does not take part (bad header, bounds, table full): slot
+// field all ones, above every real slot, so those keys sort last
+constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                        const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
+                                                        unsigned long long *__restrict__ keys, RoRec *__restrict__ recs)
+{
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t p0 = wave * 64u;
+    if (p0 >= n) return;                                       // wave-uniform
+    const uint32_t gn = (n - p0 < 64u) ? n - p0 : 64u;
+    const bool live = lane < gn;
+    const uint32_t p = p0 + (live ? lane : 0u);
+    const RawHdr raw = load_hdr(R, pkts, stride, lens, p);
+    const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
+    ParsedHdr h = parse_hdr(raw, hl, stride, live);
+    // bounds against the fragment's own bufferLength, before the lookup (the reference
+    // memcpy's unchecked at cpp:391; dropped and counted here)
+    if (h.ok && (uint64_t)h.off + h.pl > h.blen) {
+        h.ok = false;
+        h.derr = true;
+    }
+    // runs of equal keys: only the run head registers the key
+    const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(h.ev >> 32), 0u) << 32) | lane_prev((uint32_t)h.ev, 0u);
+    const uint32_t pd = lane_prev(h.d, 0u), pok = lane_prev(h.ok ? 1u : 0u, 0u);
+    const bool head = h.ok && (lane == 0 || !pok || pev != h.ev || pd != h.d);
+    const LookupResult lr = find_or_create<true>(R, head, h.ev, h.d, h.blen, now);
+    const uint64_t H = __ballot(head);
+    const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t hm = H & le;
+    const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
+    const uint32_t slot = __shfl(lr.slot, myhead);
+    if (h.ok && slot == kNoSlot) {                             // table full / probe timeout
+        h.ok = false;
+        h.derr = true;
+    }
+    if (live) {
+        keys[p] = ((unsigned long long)(h.ok ? slot : kRoNoSlot) << 32) | p;
+        const u32x4 v = {h.off, h.pl, h.blen, hl};
+        st16(reinterpret_cast<uint8_t *>(recs + p), v);
+    }
+    wave_stats(R, live, live ? raw.len : 0u, h.bad, h.derr, wave);
+}
+
+// One thread per sorted position; the first position of each key walks all of them.
+__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsigned long long *__restrict__ keys,
+                                                         const RoRec *__restrict__ recs, uint32_t n, uint64_t now,
+                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
+{
+    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
+    if (i >= n) return;
+    const unsigned long long k = keys[i];
+    const uint32_t slot = (uint32_t)(k >> 32);
+    if (slot >= R.tableSlots) {                                // takes no part: nothing to copy
+        const uint32_t q = (uint32_t)k;
+        st16(reinterpret_cast<uint8_t *>(info + q), u32x4{0u, 0u, 0u, recs[q].hl});
+        return;
+    }
+    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == slot) return;   // not the key's first position
+    ReasSlot *sl = R.slots + slot;
+    const uint64_t ev = sl->eventNum;
+    const uint32_t d = sl->dataId;
+    bool item = sl->bvalid == 1u;                              // an item in progress from an earlier batch
+    uint64_t boff = sl->bufOff;
+    uint32_t ibytes = sl->bytes;
+    uint64_t cur = item ? (sl->acc & kAccBytesMask) : 0ull;
+    uint32_t frags = item ? (uint32_t)(sl->acc >> kAccFragShift) : 0u;
+    uint64_t created = sl->created;
+    long long live = 0;                                        // net change of items in progress
+    uint32_t derr = 0;
+    for (uint32_t j = i; j < n; j++) {
+        const unsigned long long kj = keys[j];
+        if ((uint32_t)(kj >> 32) != slot) break;
+        const uint32_t q = (uint32_t)kj;
+        const RoRec rc = recs[q];
+        if (rc.off == 0u || !item) {
+            // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the one
+            // in progress in the map (cpp:361-369), which is dropped without a lost record
+            if (item) live--;
+            const uint64_t need = ((uint64_t)rc.blen + 255ull) & ~255ull;
+            boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
+            if (boff + rc.blen > R.arenaBytes) {
+                boff = kNoBuf;
+                atomicOr(&R.ctl->errorFlags, 2u);
+            }
+            ibytes = rc.blen;
+            cur = 0;
+            frags = 0;
+            created = now;
+            item = true;
+            live++;
+        }
+        PktInfo pi{0ull, 0u, rc.hl};
+        if ((uint64_t)rc.off + rc.plen > ibytes) {
+            derr++;                // the item was made by a fragment with another bufferLength
+        } else {
+            if (boff != kNoBuf) {
+                pi.dst = (uint64_t)(R.arena + boff + rc.off);
+                pi.plen = rc.plen;
+            }
+            frags++;                                           // cpp:398-400
+            cur += rc.plen;
+            if (cur == ibytes) {                               // cpp:403: complete, erase, enqueue
+                FinishRec f;
+                f.ev = ev;
+                f.boff = boff;
+                f.slot = slot | kFinKeepSlot;
+                f.bytes = ibytes;
+                f.frags = frags;
+                f.d = d;
+                fin[q] = f;
+                pi.hl |= kPktCompletes;
+                item = false;                                  // inProgress-- in complete_event
+            }
+        }
+        st16(reinterpret_cast<uint8_t *>(info + q), u32x4{(uint32_t)pi.dst, (uint32_t)(pi.dst >> 32), pi.plen, pi.hl});
+    }
+    if (item) {
+        sl->bufOff = boff;
+        sl->bytes = ibytes;
+        sl->bvalid = 1u;
+        sl->acc = ((unsigned long long)frags << kAccFragShift) | (cur & kAccBytesMask);
+        sl->created = created;
+    } else {
+        sl->state = kDone;                                     // no item left under this key
+    }
+    if (live) atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), (unsigned long long)live);
+    if (derr) atomicAdd(&R.shards[slot % kShards].dataErrCnt, (unsigned long long)derr);
 }
 
 // Zero nWords dwords.  Used instead of hipMemsetAsync wherever the launch may be captured
@@ -1406,6 +1618,24 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
+    return hipGetLastError();
+}
+
+hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                              uint32_t n, uint64_t now, void *work, void *scratch, size_t scratchBytes,
+                              hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    uint8_t *w = static_cast<uint8_t *>(work);
+    RoScratch sc = ro_scratch_layout(scratch, n);
+    if (ro_scratch_bytes(n, R.tableSlots) > scratchBytes) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
+                       sc.keysIn, sc.recs);
+    size_t tb = scratchBytes - (size_t)(sc.temp - static_cast<uint8_t *>(scratch));
+    hipError_t e = ro_sort_keys(sc.temp, tb, sc.keysIn, sc.keysOut, n, ro_sort_end_bit(R.tableSlots), stream);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, sc.keysOut, sc.recs, n,
+                       now, reinterpret_cast<PktInfo *>(w), reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
 

@@ -105,6 +105,43 @@ static_assert(sizeof(FinishRec) == 32, "two dwordx4 per record");
 inline size_t work_fin_off(uint32_t n) { return ((size_t)n * sizeof(PktInfo) + 255) & ~(size_t)255; }
 inline size_t work_bytes(uint32_t n) { return work_fin_off(n) + (size_t)n * sizeof(FinishRec); }
 
+// Reference-order mode: per-datagram record of ro_key_kernel, and the scratch it needs
+// (sort keys in and out, records, rocPRIM temporary storage) for a batch of n datagrams.
+struct RoRec {
+    uint32_t off, plen, blen, hl;
+};
+static_assert(sizeof(RoRec) == 16, "one dwordx4 per datagram");
+struct RoScratch {
+    unsigned long long *keysIn, *keysOut;
+    RoRec *recs;
+    uint8_t *temp;
+};
+inline size_t ro_align(size_t x) { return (x + 255) & ~(size_t)255; }
+inline RoScratch ro_scratch_layout(void *base, uint32_t n)
+{
+    uint8_t *b = static_cast<uint8_t *>(base);
+    RoScratch s;
+    s.keysIn = reinterpret_cast<unsigned long long *>(b);
+    s.keysOut = reinterpret_cast<unsigned long long *>(b + ro_align(8ull * n));
+    s.recs = reinterpret_cast<RoRec *>(b + 2 * ro_align(8ull * n));
+    s.temp = b + 2 * ro_align(8ull * n) + ro_align(16ull * n);
+    return s;
+}
+// sort bits: slot (< tableSlots = 2^t) above the 32-bit position, plus the all-ones "no
+// slot" marker's bit t
+inline unsigned ro_sort_end_bit(uint32_t tableSlots)
+{
+    unsigned t = 0;
+    while ((1u << t) < tableSlots) t++;
+    return 33u + t;
+}
+hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long *in, unsigned long long *out,
+                        uint32_t n, unsigned endBit, hipStream_t stream);   // temp == nullptr: size query
+size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots);
+hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                              uint32_t n, uint64_t now, void *work, void *scratch, size_t scratchBytes,
+                              hipStream_t stream);
+
 // d_count (optional): the event count is read on the device; nEvents is then its bound
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,

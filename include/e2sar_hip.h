@@ -142,6 +142,19 @@ typedef struct e2sar_hip_reas_config {
 /* Allocate a second table + arena so e2sar_hip_reas_compact() can move in-progress
  * events out of a full arena (streaming use: events that straddle batches). */
 #define E2SAR_HIP_REAS_COMPACTABLE 1u
+/* Reassemble with the reference receive body's arrival-order rules, whatever the order:
+ * a fragment with bufferOffset 0 always starts a new item, dropping an item in progress
+ * under the same (eventNum, dataId) without a lost record (e2sarDPReassembler.cpp:361-369);
+ * a fragment whose key has no item starts one, also after its event completed
+ * (cpp:376-384); completion is tested after every fragment (cpp:403), so duplicates
+ * before the last fragment overshoot curBytes.  Arrival order = batch order, then datagram
+ * order in the batch.  Without the flag the device path is order-insensitive: every
+ * fragment joins its event and completion is tested per run of a launch (identical results
+ * whenever offset 0 arrives first and there are no duplicates).  The mode
+ * adds a key sort per batch and device scratch that grows on demand (a launch that grows it
+ * synchronises the device, so capture a HIP graph only after a first batch of the largest
+ * size has run). */
+#define E2SAR_HIP_REAS_REFERENCE_ORDER 2u
 
 /* Reassembled event handed to the caller (getEvent's out-params, cpp:626-641).
  * The bytes live at e2sar_hip_reas_arena() + arenaOffset until the arena is recycled. */
@@ -226,14 +239,16 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride,
  * (reassemblyLoss, cpp:252-274).  Asynchronous. */
 int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, void *stream);
 
-/* Drain completed events (synchronises the stream).  Records are returned in
- * completion order of the device; *nOut <= cap.  Records beyond cap stay queued. */
+/* Drain completed events.  Synchronises the device (every stream: launches may have used
+ * any stream) under the reassembler's lock, so no kernel of this reassembler runs while
+ * the list is drained.  Records are returned in completion order of the device;
+ * *nOut <= cap.  Records beyond cap stay queued. */
 int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t cap,
                         uint32_t *nOut);
-/* Drain lost-event records (synchronises). */
+/* Drain lost-event records (synchronises the device, as reas_poll). */
 int e2sar_hip_reas_lost_poll(e2sar_hip_reas *r, e2sar_hip_lost_rec *out, uint32_t cap,
                              uint32_t *nOut);
-/* Stats snapshot (synchronises). */
+/* Stats snapshot (synchronises the device, as reas_poll). */
 int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out);
 /* Recycle the arena and the event table.  Only legal when no event is in progress
  * and every completed record has been polled (else E2SAR_HIP_ERR_LOGIC); the caller
@@ -246,7 +261,8 @@ int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream);
  * polled (their arena offsets refer to the old arena; copy the bytes out first).
  * Asynchronous; e2sar_hip_reas_arena() returns the new base afterwards. */
 int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream);
-/* Zero every counter and the lost/completion lists (asynchronous). */
+/* Zero the statistics counters (event counters, per-datagram counters, error flags).
+ * Completed and lost records not yet polled stay queued.  Asynchronous. */
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
 
 /* ------------------------------------------------------------------ */

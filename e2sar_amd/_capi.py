@@ -128,6 +128,13 @@ SIGNATURES = {
     "e2sar_hip_memset_d": (i, [vp, vp, i, sz]),
     "e2sar_hip_memcpy_async": (i, [vp, vp, vp, sz, i, vp]),
     "e2sar_hip_stream_sync": (i, [vp, vp]),
+    "e2sar_hip_event_create": (i, [vp, C.POINTER(vp)]),
+    "e2sar_hip_event_destroy": (i, [vp]),
+    "e2sar_hip_event_record": (i, [vp, vp, vp]),
+    "e2sar_hip_stream_wait_event": (i, [vp, vp, vp]),
+    "e2sar_hip_event_query": (i, [vp]),
+    "e2sar_hip_event_sync": (i, [vp]),
+    "e2sar_hip_copy_spans": (i, [vp, vp, u32, vp]),
     "e2sar_hip_total_hdr_len": (sz, [i]),
     "e2sar_hip_max_pld_len": (sz, [u32, i]),
     "e2sar_hip_num_packets": (sz, [sz, sz]),

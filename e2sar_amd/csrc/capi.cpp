@@ -230,6 +230,75 @@ int e2sar_hip_stream_sync(e2sar_hip_ctx *ctx, void *stream)
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_event_create(e2sar_hip_ctx *ctx, void **out)
+{
+    if (!ctx || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *out = e;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_event_destroy(void *event)
+{
+    if (event) HIP_TRY(hipEventDestroy(static_cast<hipEvent_t>(event)));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_event_record(e2sar_hip_ctx *ctx, void *event, void *stream)
+{
+    if (!ctx || !event) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(event), stream ? static_cast<hipStream_t>(stream) : ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_stream_wait_event(e2sar_hip_ctx *ctx, void *stream, void *event)
+{
+    if (!ctx || !event) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    HIP_TRY(hipStreamWaitEvent(stream ? static_cast<hipStream_t>(stream) : ctx->stream, static_cast<hipEvent_t>(event), 0));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_event_query(void *event)
+{
+    if (!event) return fail(E2SAR_HIP_ERR_PARAMETER, "event is NULL");
+    const hipError_t e = hipEventQuery(static_cast<hipEvent_t>(event));
+    if (e == hipSuccess) return 1;
+    if (e == hipErrorNotReady) return 0;
+    return hip_fail(e, "hipEventQuery");
+}
+
+int e2sar_hip_event_sync(void *event)
+{
+    if (!event) return fail(E2SAR_HIP_ERR_PARAMETER, "event is NULL");
+    HIP_TRY(hipEventSynchronize(static_cast<hipEvent_t>(event)));
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_copy_spans(e2sar_hip_ctx *ctx, const e2sar_hip_copy_span *spans, uint32_t n, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (n == 0) return E2SAR_HIP_OK;
+    if (!spans) return fail(E2SAR_HIP_ERR_PARAMETER, "spans is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    for (uint32_t i0 = 0; i0 < n; i0 += kCopySpansPerLaunch) {
+        CopySpans cs{};
+        cs.n = std::min<uint32_t>(kCopySpansPerLaunch, n - i0);
+        uint64_t most = 0;
+        for (uint32_t k = 0; k < cs.n; k++) {
+            const auto &sp = spans[i0 + k];
+            if (sp.bytes && (!sp.src || !sp.dst)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL span pointer");
+            cs.s[k] = CopySpan{reinterpret_cast<uint64_t>(sp.src), reinterpret_cast<uint64_t>(sp.dst), sp.bytes};
+            most = std::max<uint64_t>(most, sp.bytes);
+        }
+        hipError_t e = launch_copy_spans(cs, most, s);
+        if (e != hipSuccess) return hip_fail(e, "copy_spans launch");
+    }
+    return E2SAR_HIP_OK;
+}
+
 /* ---------------- geometry ---------------- */
 
 size_t e2sar_hip_total_hdr_len(int useIPv6)

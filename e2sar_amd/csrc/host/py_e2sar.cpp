@@ -263,6 +263,7 @@ PYBIND11_MODULE(e2sar_py, m)
     seg.def("getSyncStats", &Segmenter::getSyncStats);
     seg.def("getMTU", &Segmenter::getMTU);
     seg.def("getMaxPldLen", &Segmenter::getMaxPldLen);
+    seg.def("getIntf", &Segmenter::getIntf);
     seg.def("stopThreads", [](Segmenter &s) {
         py::gil_scoped_release rel;
         s.stopThreads();
@@ -289,7 +290,9 @@ PYBIND11_MODULE(e2sar_py, m)
         .def_readwrite("max_factor", &ReassemblerFlagsT::max_factor)
         .def_readwrite("gpuDevice", &ReassemblerFlagsT::gpuDevice)
         .def_readwrite("recvBatch", &ReassemblerFlagsT::recvBatch)
+        .def_readwrite("referenceOrder", &ReassemblerFlagsT::referenceOrder)
         .def_readwrite("recvStride", &ReassemblerFlagsT::recvStride)
+        .def_readwrite("tableSlots", &ReassemblerFlagsT::tableSlots)
         .def_readwrite("arenaBytes", &ReassemblerFlagsT::arenaBytes)
         .def_readwrite("batchTimeout_us", &ReassemblerFlagsT::batchTimeout_us)
         .def_static("getFromINI", &ReassemblerFlagsT::getFromINI);
@@ -380,6 +383,13 @@ PYBIND11_MODULE(e2sar_py, m)
         .def_readonly("badHeaderDiscards", &Reassembler::ReportedStats::badHeaderDiscards);
     reas.def("getStats", &Reassembler::getStats);
     reas.def("get_dataIP", &Reassembler::get_dataIP);
+    py::class_<Reassembler::DeviceStats>(reas, "DeviceStats")
+        .def_readonly("tableUsed", &Reassembler::DeviceStats::tableUsed)
+        .def_readonly("arenaUsed", &Reassembler::DeviceStats::arenaUsed)
+        .def_readonly("upkeeps", &Reassembler::DeviceStats::upkeeps)
+        .def_readonly("inProgress", &Reassembler::DeviceStats::inProgress)
+        .def_readonly("errorFlags", &Reassembler::DeviceStats::errorFlags);
+    reas.def("getDeviceStats", &Reassembler::getDeviceStats);
     reas.def("get_numRecvThreads", &Reassembler::get_numRecvThreads);
     reas.def("get_recvPorts", &Reassembler::get_recvPorts);
     reas.def("get_portRange", &Reassembler::get_portRange);

@@ -4,11 +4,14 @@
 // (e2sarDPReassembler.cpp:293-433) -- malloc, recvfrom, header checks, map lookup, memcpy
 // -- one datagram at a time; a GC thread drops stale events (cpp:236-291).
 // Here the receive threads only fill pinned datagram batches with recvmmsg (a slot of
-// recvStride bytes per datagram); one device thread moves each full (or timed-out)
-// batch to HBM and runs reas_kernel on it, then drains completed events (device ->
-// new[] host buffers -> the event queue that getEvent/recvEvent read) and lost-event
-// records, runs the device GC pass every eventTimeout_ms, and compacts the device arena
-// when it fills.  Event bytes are copied to the caller's new[] buffer exactly once.
+// recvStride bytes per datagram); one device thread pipelines the batches through HBM:
+// the host->device copy of batch b+1 runs on a copy stream beside the reassembly kernel of
+// batch b (two device datagram buffers), a host batch goes back to the receive threads as
+// soon as its copy has landed, and the events batch b completed leave the device arena in
+// ONE gather launch into pinned staging, from which they are copied into the new[] buffers
+// that getEvent/recvEvent hand over.  Lost-event records are drained the same way; the
+// device GC pass runs every eventTimeout_ms; the table and arena are recycled or compacted
+// when either passes half full.
 #include <arpa/inet.h>
 #include <netinet/in.h>
 #include <poll.h>
@@ -43,12 +46,23 @@ struct Reassembler::Impl {
     size_t numRecvPorts;
     std::vector<std::vector<uint16_t>> threadsToPorts;
 
-    // device
+    // device: the compute stream (the context's) and a copy stream; two device datagram
+    // buffers so batch b+1 is copied in while batch b is reassembled
     e2sar_hip_ctx *ctx = nullptr;
     void *stream = nullptr;
+    void *copyStream = nullptr;
     e2sar_hip_reas *reas = nullptr;
-    uint8_t *dPkts = nullptr;
-    uint32_t *dLens = nullptr;
+    struct DevSet {
+        uint8_t *pkts = nullptr;
+        uint32_t *lens = nullptr;
+        void *h2dDone = nullptr;        // recorded on the copy stream after the batch's copy
+    };
+    DevSet sets[2];
+    void *gatherDone = nullptr;         // recorded on the compute stream after a drain's gather
+    uint8_t *stage = nullptr;           // pinned staging for completed events
+    size_t stageBytes = 0;
+    std::vector<size_t> stageOffs;      // staging offsets of the records of the gather in flight
+    std::atomic<uint64_t> upkeeps{0};   // recycles + compactions done
     std::vector<e2sar_hip_event_rec> recs;
     std::vector<e2sar_hip_lost_rec> lrecs;
 
@@ -98,24 +112,39 @@ struct Reassembler::Impl {
     void setup(size_t nThreads);
     void recvBody(size_t t, std::vector<int> fds, std::vector<uint16_t> ports);
     void devBody();
-    void drain(bool all);
+    void drainLost();
+    uint32_t gatherLaunch(uint32_t first, uint32_t n, uint8_t *arena);
+    void gatherFinish(uint32_t first, uint32_t upto);
+    bool needsUpkeep(const e2sar_hip_reas_stats &st) const;
+    void upkeep(const e2sar_hip_reas_stats &st);
     Batch *takeFree();
+    Batch *takeFull(bool wait);
+    void giveBack(Batch *b);
 };
 
 Reassembler::Impl::~Impl()
 {
-    if (ctx) e2sar_hip_stream_sync(ctx, stream);
+    if (ctx) {
+        e2sar_hip_stream_sync(ctx, stream);
+        e2sar_hip_stream_sync(ctx, copyStream);
+    }
     for (auto &b : batches) {
         if (b.pkts) e2sar_hip_host_free(b.pkts);
         if (b.lens) e2sar_hip_host_free(b.lens);
     }
+    if (stage) e2sar_hip_host_free(stage);
     if (reas) e2sar_hip_reas_destroy(reas);
     if (ctx) {
-        if (dPkts) e2sar_hip_device_free(ctx, dPkts);
-        if (dLens) e2sar_hip_device_free(ctx, dLens);
+        for (auto &d : sets) {
+            if (d.pkts) e2sar_hip_device_free(ctx, d.pkts);
+            if (d.lens) e2sar_hip_device_free(ctx, d.lens);
+            e2sar_hip_event_destroy(d.h2dDone);
+        }
+        e2sar_hip_event_destroy(gatherDone);
         e2sar_hip_ctx_destroy(ctx);
     }
     if (stream) e2sar_hip_stream_destroy(stream);
+    if (copyStream) e2sar_hip_stream_destroy(copyStream);
     std::lock_guard<std::mutex> lk(eMu);
     for (auto &e : evq) delete[] e.event;
 }
@@ -140,6 +169,7 @@ void Reassembler::Impl::setup(size_t nThreads)
     }
 
     int rc = e2sar_hip_stream_create(flags.gpuDevice, &stream);
+    if (rc == 0) rc = e2sar_hip_stream_create(flags.gpuDevice, &copyStream);
     if (rc == 0) rc = e2sar_hip_ctx_create(flags.gpuDevice, stream, &ctx);
     e2sar_hip_reas_config cfg{};
     cfg.withLBHeader = flags.withLBHeader ? 1 : 0;
@@ -147,10 +177,16 @@ void Reassembler::Impl::setup(size_t nThreads)
     cfg.queueCapacity = (uint32_t)std::max<size_t>(4096, flags.recvBatch);
     cfg.lostCapacity = 4096;
     cfg.arenaBytes = flags.arenaBytes;
-    cfg.flags = E2SAR_HIP_REAS_COMPACTABLE;
+    cfg.flags = E2SAR_HIP_REAS_COMPACTABLE | (flags.referenceOrder ? E2SAR_HIP_REAS_REFERENCE_ORDER : 0u);
     if (rc == 0) rc = e2sar_hip_reas_create(ctx, &cfg, &reas);
-    if (rc == 0) rc = e2sar_hip_device_alloc(ctx, flags.recvBatch * flags.recvStride, reinterpret_cast<void **>(&dPkts));
-    if (rc == 0) rc = e2sar_hip_device_alloc(ctx, flags.recvBatch * 4, reinterpret_cast<void **>(&dLens));
+    for (auto &d : sets) {
+        if (rc == 0) rc = e2sar_hip_device_alloc(ctx, flags.recvBatch * flags.recvStride, reinterpret_cast<void **>(&d.pkts));
+        if (rc == 0) rc = e2sar_hip_device_alloc(ctx, flags.recvBatch * 4, reinterpret_cast<void **>(&d.lens));
+        if (rc == 0) rc = e2sar_hip_event_create(ctx, &d.h2dDone);
+    }
+    if (rc == 0) rc = e2sar_hip_event_create(ctx, &gatherDone);
+    stageBytes = std::max<size_t>(size_t(64) << 20, 2 * flags.recvBatch * flags.recvStride);
+    if (rc == 0) rc = e2sar_hip_host_alloc(stageBytes, reinterpret_cast<void **>(&stage));
     const size_t nb = 2 * numRecvThreads + 2;
     batches.resize(nb);
     for (auto &b : batches) {
@@ -298,24 +334,76 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
     }
 }
 
-// Drain completed events (device records -> new[] buffers -> event queue) and lost records.
-void Reassembler::Impl::drain(bool)
+Reassembler::Impl::Batch *Reassembler::Impl::takeFull(bool wait)
 {
-    uint32_t n = 0;
-    if (e2sar_hip_reas_poll(reas, recs.data(), (uint32_t)recs.size(), &n) != 0) {
+    std::unique_lock<std::mutex> lk(bMu);
+    if (wait) bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
+    if (fullB.empty()) return nullptr;
+    Batch *b = fullB.front();
+    fullB.pop_front();
+    return b;
+}
+
+void Reassembler::Impl::giveBack(Batch *b)
+{
+    {
+        std::lock_guard<std::mutex> lk(bMu);
+        freeB.push_back(b);
+    }
+    bFreeCv.notify_all();
+}
+
+// Completed records recs[first, n) (already polled; their bytes in `arena`) -> pinned
+// staging, as many as fit, in one gather launch (e2sar_hip_copy_spans) on the compute
+// stream, so it runs ahead of any later kernel or recycle that could overwrite them.
+// Returns the index past the last record launched; gatherFinish waits for that launch and
+// copies the events into the new[] buffers the caller will own (bin/e2sar_perf.cpp:299).
+uint32_t Reassembler::Impl::gatherLaunch(uint32_t first, uint32_t n, uint8_t *arena)
+{
+    stageOffs.clear();
+    std::vector<e2sar_hip_copy_span> spans;
+    size_t used = 0;
+    uint32_t i = first;
+    for (; i < n; i++) {
+        const size_t b = recs[i].bytes;
+        const size_t need = (b + 63) & ~(size_t)63;
+        if (need > stageBytes && i == first) {          // larger than all of the staging: grow it
+            e2sar_hip_stream_sync(ctx, stream);
+            e2sar_hip_host_free(stage);
+            stage = nullptr;
+            stageBytes = 0;
+            if (e2sar_hip_host_alloc(need, reinterpret_cast<void **>(&stage)) != 0) {
+                lastErr = E2SARErrorc::MemoryError;
+                return n;
+            }
+            stageBytes = need;
+        }
+        if (used + need > stageBytes) break;
+        stageOffs.push_back(used);
+        if (b) spans.push_back(e2sar_hip_copy_span{arena + recs[i].arenaOffset, stage + used, b});
+        used += need;
+    }
+    int rc = e2sar_hip_copy_spans(ctx, spans.data(), (uint32_t)spans.size(), stream);
+    if (rc == 0) rc = e2sar_hip_event_record(ctx, gatherDone, stream);
+    if (rc) lastErr = E2SARErrorc::SystemError;
+    return i;
+}
+
+void Reassembler::Impl::gatherFinish(uint32_t first, uint32_t upto)
+{
+    if (upto <= first) return;
+    if (e2sar_hip_event_sync(gatherDone) != 0 || stageOffs.size() != upto - first) {
         lastErr = E2SARErrorc::SystemError;
         return;
     }
-    uint8_t *arena = e2sar_hip_reas_arena(reas);
     std::vector<Ev> ready;
-    ready.reserve(n);
-    for (uint32_t i = 0; i < n; i++) {
-        const auto &r = recs[i];
+    ready.reserve(upto - first);
+    for (uint32_t k = first; k < upto; k++) {
+        const auto &r = recs[k];
         auto *buf = new uint8_t[r.bytes ? r.bytes : 1];
-        if (r.bytes) e2sar_hip_memcpy_async(ctx, buf, arena + r.arenaOffset, r.bytes, 1, nullptr);
+        if (r.bytes) memcpy(buf, stage + stageOffs[k - first], r.bytes);
         ready.push_back(Ev{buf, r.bytes, r.eventNum, r.dataId});
     }
-    if (n) e2sar_hip_stream_sync(ctx, nullptr);
     {
         std::lock_guard<std::mutex> lk(eMu);
         for (auto &e : ready) {
@@ -329,7 +417,11 @@ void Reassembler::Impl::drain(bool)
             }
         }
     }
-    if (n) eCv.notify_all();
+    eCv.notify_all();
+}
+
+void Reassembler::Impl::drainLost()
+{
     uint32_t nl = 0;
     if (e2sar_hip_reas_lost_poll(reas, lrecs.data(), (uint32_t)lrecs.size(), &nl) == 0 && nl) {
         std::lock_guard<std::mutex> l2(lMu);
@@ -340,57 +432,108 @@ void Reassembler::Impl::drain(bool)
     }
 }
 
+// Recycle or compact once the arena or the table is half used.  Completed and timed-out
+// slots keep their table entries until then, so with small events and a steady stream
+// the table fills long before the arena; compaction keeps only the events in progress.
+// It is skipped when it would not free at least half of the table (most slots live).
+// Runs with the device idle and every completed record polled and gathered.
+bool Reassembler::Impl::needsUpkeep(const e2sar_hip_reas_stats &st) const
+{
+    if (st.completedPending != 0) return false;
+    const bool arenaHalf = st.arenaUsed > flags.arenaBytes / 2;
+    const bool tableHalf = st.tableUsed > flags.tableSlots / 2 &&
+                           st.tableUsed > 2 * (uint64_t)std::max<int64_t>(st.inProgress, 0);
+    return arenaHalf || tableHalf;
+}
+
+void Reassembler::Impl::upkeep(const e2sar_hip_reas_stats &st)
+{
+    const int rc = st.inProgress == 0 ? e2sar_hip_reas_recycle(reas, 0, nullptr) : e2sar_hip_reas_compact(reas, nullptr);
+    if (rc) lastErr = static_cast<E2SARErrorc>(-rc);
+    else upkeeps++;
+}
+
+// The device thread.  Per batch b (two device buffers, sets[b % 2]):
+//   copy b+1 in (copy stream, beside kernel b) -> poll b (waits for kernel b and the copy)
+//   -> hand b+1's host batch back -> stats (device idle) -> gather b's events (compute
+//   stream) -> [GC pass / recycle / compact, before any later kernel] -> kernel b+1
+//   (after the copy's event) -> host copies of b's events while kernel b+1 runs.
 void Reassembler::Impl::devBody()
 {
     uint64_t lastGc = detail::steady_ms();
+    const uint32_t stride = (uint32_t)flags.recvStride;
+    bool kernelInFlight = false;       // a launched batch whose results are not yet drained
+    int cur = 0;                       // device set of the next copy
     while (true) {
-        Batch *b = nullptr;
-        {
-            std::unique_lock<std::mutex> lk(bMu);
-            bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
-            if (!fullB.empty()) {
-                b = fullB.front();
-                fullB.pop_front();
-            } else if (stop && recvActive.load() == 0) {
-                break;
+        Batch *b = takeFull(!kernelInFlight);
+        if (!b && !kernelInFlight && stop && recvActive.load() == 0) {
+            std::lock_guard<std::mutex> lk(bMu);
+            if (fullB.empty()) break;
+        }
+        DevSet &d = sets[cur];
+        uint32_t bn = 0;
+        uint64_t bnow = 0;
+        if (b) {
+            bn = b->n;
+            bnow = detail::steady_ms();
+            int rc = e2sar_hip_memcpy_async(ctx, d.pkts, b->pkts, (size_t)b->n * stride, 0, copyStream);
+            if (rc == 0) rc = e2sar_hip_memcpy_async(ctx, d.lens, b->lens, (size_t)b->n * 4, 0, copyStream);
+            if (rc == 0) rc = e2sar_hip_event_record(ctx, d.h2dDone, copyStream);
+            if (rc) lastErr = static_cast<E2SARErrorc>(-rc);
+        }
+        uint32_t n = 0;
+        if (e2sar_hip_reas_poll(reas, recs.data(), (uint32_t)recs.size(), &n) != 0) lastErr = E2SARErrorc::SystemError;
+        if (b) giveBack(b);                                   // its bytes are on the device now
+        kernelInFlight = false;
+        e2sar_hip_reas_stats st{};
+        const bool haveStats = e2sar_hip_reas_get_stats(reas, &st) == 0;
+        if (haveStats) {
+            std::lock_guard<std::mutex> lk(sMu);
+            lastStats = st;
+        }
+        uint8_t *arena = e2sar_hip_reas_arena(reas);
+        uint32_t upto = n ? gatherLaunch(0, n, arena) : 0;
+        const uint64_t now = detail::steady_ms();
+        const bool gcDue = now - lastGc >= (uint64_t)flags.eventTimeout_ms;
+        const bool upkeepDue = haveStats && needsUpkeep(st);
+        uint32_t done = 0;
+        if (gcDue || upkeepDue) {
+            // every completed event leaves the arena before the GC pass, a recycle or a compaction
+            for (gatherFinish(0, upto), done = upto; done < n; done = upto) {
+                upto = gatherLaunch(done, n, arena);
+                gatherFinish(done, upto);
             }
+            if (gcDue) {                              // GC thread period (cpp:252-283)
+                e2sar_hip_reas_gc(reas, now, (uint64_t)flags.eventTimeout_ms, nullptr);
+                lastGc = now;
+                drainLost();
+            }
+            if (upkeepDue) upkeep(st);
         }
         if (b) {
-            const uint64_t now = detail::steady_ms();
-            int rc = e2sar_hip_memcpy_async(ctx, dPkts, b->pkts, (size_t)b->n * flags.recvStride, 0, nullptr);
-            if (rc == 0) rc = e2sar_hip_memcpy_async(ctx, dLens, b->lens, (size_t)b->n * 4, 0, nullptr);
-            if (rc == 0) rc = e2sar_hip_reassemble_batch(reas, dPkts, (uint32_t)flags.recvStride, dLens, b->n, now, nullptr);
-            if (rc == 0) rc = e2sar_hip_stream_sync(ctx, nullptr);
+            int rc = e2sar_hip_stream_wait_event(ctx, nullptr, d.h2dDone);
+            if (rc == 0) rc = e2sar_hip_reassemble_batch(reas, d.pkts, stride, d.lens, bn, bnow, nullptr);
             if (rc) lastErr = static_cast<E2SARErrorc>(-rc);
-            {
-                std::lock_guard<std::mutex> lk(bMu);
-                freeB.push_back(b);
-            }
-            bFreeCv.notify_all();
-            drain(false);
+            else kernelInFlight = true;
+            cur ^= 1;
         }
-        const uint64_t now = detail::steady_ms();
-        if (now - lastGc >= (uint64_t)flags.eventTimeout_ms) {    // GC thread period (cpp:252-283)
-            e2sar_hip_reas_gc(reas, now, (uint64_t)flags.eventTimeout_ms, nullptr);
-            lastGc = now;
-            drain(false);
-        }
-        e2sar_hip_reas_stats st{};
-        if (e2sar_hip_reas_get_stats(reas, &st) == 0) {
-            {
-                std::lock_guard<std::mutex> lk(sMu);
-                lastStats = st;
-            }
-            // recycle or compact the arena once half of it is used (no completed record pending)
-            if (st.completedPending == 0 && st.arenaUsed > flags.arenaBytes / 2) {
-                if (st.inProgress == 0) e2sar_hip_reas_recycle(reas, 0, nullptr);
-                else e2sar_hip_reas_compact(reas, nullptr);
-            } else if (st.completedPending == 0 && st.inProgress == 0 && st.tableUsed > flags.tableSlots / 2) {
-                e2sar_hip_reas_recycle(reas, 0, nullptr);
+        if (done < n) {                                // while that kernel runs
+            gatherFinish(done, upto);
+            for (done = upto; done < n; done = upto) {
+                upto = gatherLaunch(done, n, arena);
+                gatherFinish(done, upto);
             }
         }
     }
-    drain(true);
+    uint32_t n = 0;
+    if (e2sar_hip_reas_poll(reas, recs.data(), (uint32_t)recs.size(), &n) == 0 && n) {
+        uint8_t *arena = e2sar_hip_reas_arena(reas);
+        for (uint32_t done = 0, upto; done < n; done = upto) {
+            upto = gatherLaunch(done, n, arena);
+            gatherFinish(done, upto);
+        }
+    }
+    drainLost();
 }
 
 result<int> Reassembler::registerWorker(const std::string &) noexcept
@@ -538,6 +681,17 @@ const std::pair<int, int> Reassembler::get_recvPorts() const noexcept
 }
 int Reassembler::get_portRange() const noexcept { return impl->portRange; }
 const std::string Reassembler::get_dataIP() const noexcept { return impl->dataIP; }
+
+const Reassembler::DeviceStats Reassembler::getDeviceStats() const noexcept
+{
+    auto &m = *impl;
+    e2sar_hip_reas_stats st{};
+    if (!m.started || e2sar_hip_reas_get_stats(m.reas, &st) != 0) {
+        std::lock_guard<std::mutex> lk(m.sMu);
+        st = m.lastStats;
+    }
+    return DeviceStats{st.tableUsed, st.arenaUsed, m.upkeeps.load(), st.inProgress, st.errorFlags};
+}
 
 void Reassembler::stopThreads()
 {

@@ -38,6 +38,7 @@ struct Segmenter::Impl {
     std::vector<int> cores;
     bool useV6 = false;
     uint16_t mtu = 1500;
+    std::string iface;               // outgoing interface of the data address (getIntf)
     size_t maxPld = 0;
     uint32_t stride = 0;
 
@@ -154,7 +155,30 @@ static void init_impl(Segmenter::Impl &m)
 {
     m.useV6 = m.flags.dpV6 && m.uri.has_dataAddrv6();
     if (!m.uri.has_dataAddrv4() && m.uri.has_dataAddrv6()) m.useV6 = true;
-    m.mtu = m.flags.mtu ? m.flags.mtu : 1500;   // mtu 0 (netlink auto-detect) -> 1500 here
+    // outgoing interface and its MTU for the URI's data address (e2sarDPSegmenter.cpp:56-110):
+    // mtu 0 takes the interface's MTU, an override must not exceed it (an interface that
+    // reports 0 accepts any override).  The device slot layout is sized for the
+    // reference's 9000-byte limit, so an auto-detected MTU above it (loopback reports
+    // 65536) is capped at 9000.
+    auto addr = m.useV6 ? m.uri.get_dataAddrv6() : m.uri.get_dataAddrv4();
+    if (addr.has_error()) throw E2SARException("Data address is not present in the URI");
+    auto intf = NetUtil::getInterfaceAndMTU(addr.value().first);
+    uint16_t ifMtu = 0;
+    if (intf.has_value()) {
+        m.iface = std::get<0>(intf.value());
+        ifMtu = std::get<1>(intf.value());
+    } else if (m.flags.mtu == 0) {
+        throw E2SARException("Unable to determine outgoing interface for LB destination address " +
+                             addr.value().first + ": " + intf.error().message());
+    }
+    if (m.flags.mtu == 0) {
+        if (ifMtu == 0) throw E2SARException("Outgoing interface MTU is reported as 0, please use manual override of MTU size");
+        m.mtu = std::min<uint16_t>(ifMtu, 9000);
+    } else {
+        if (ifMtu > 0 && m.flags.mtu > ifMtu)
+            throw E2SARException("Segmenter flags MTU override value exceeds outgoing interface MTU of " + m.iface);
+        m.mtu = m.flags.mtu;
+    }
     m.sanity();
     m.maxPld = e2sar_hip_max_pld_len(m.mtu, m.useV6 ? 1 : 0);     // cpp:113
     m.addEntropy = !(detail::clock_entropy_bits() > kMinClockEntropy);   // cpp:50
@@ -553,7 +577,7 @@ const Segmenter::ReportedStats Segmenter::getSyncStats() const noexcept
                          E2SARErrorc::NoError};
 }
 
-const std::string Segmenter::getIntf() const noexcept { return std::string(); }
+const std::string Segmenter::getIntf() const noexcept { return impl->iface; }
 uint16_t Segmenter::getMTU() const noexcept { return impl->mtu; }
 size_t Segmenter::getMaxPldLen() const noexcept { return impl->maxPld; }
 bool Segmenter::isUsingIPv6() const noexcept { return impl->useV6; }

@@ -1,4 +1,11 @@
 // util.cpp -- EjfatURI (data-path subset), get_PortRange, INI flag loading.
+#include <ifaddrs.h>
+#include <net/if.h>
+#include <sys/ioctl.h>
+#include <arpa/inet.h>
+#include <netinet/in.h>
+#include <sys/socket.h>
+#include <unistd.h>
 #include <algorithm>
 #include <cctype>
 #include <chrono>
@@ -228,6 +235,9 @@ result<ReassemblerFlagsT> ReassemblerFlagsT::getFromINI(const std::string &iniFi
     f.gpuDevice = (int)detail::ini_num(m, "device.gpuDevice", f.gpuDevice);
     f.recvBatch = (size_t)detail::ini_num(m, "device.recvBatch", (double)f.recvBatch);
     f.arenaBytes = (size_t)detail::ini_num(m, "device.arenaBytes", (double)f.arenaBytes);
+    f.recvStride = (size_t)detail::ini_num(m, "device.recvStride", (double)f.recvStride);
+    f.tableSlots = (uint32_t)detail::ini_num(m, "device.tableSlots", (double)f.tableSlots);
+    f.referenceOrder = detail::ini_num(m, "device.referenceOrder", f.referenceOrder ? 1.0 : 0.0) != 0.0;
     return f;
 }
 
@@ -261,6 +271,65 @@ result<std::string> getHostName() noexcept
     buf[sizeof(buf) - 1] = 0;
     return std::string(buf);
 }
+result<std::tuple<std::string, uint16_t>> getInterfaceAndMTU(const std::string &ip) noexcept
+{
+    const bool v6 = ip.find(':') != std::string::npos;
+    sockaddr_storage ss{};
+    socklen_t sl;
+    if (v6) {
+        auto *a = reinterpret_cast<sockaddr_in6 *>(&ss);
+        a->sin6_family = AF_INET6;
+        a->sin6_port = htons(9);
+        if (inet_pton(AF_INET6, ip.c_str(), &a->sin6_addr) != 1) return E2SARErrorInfo{E2SARErrorc::ParameterError, "bad IPv6 address " + ip};
+        sl = sizeof(sockaddr_in6);
+    } else {
+        auto *a = reinterpret_cast<sockaddr_in *>(&ss);
+        a->sin_family = AF_INET;
+        a->sin_port = htons(9);
+        if (inet_pton(AF_INET, ip.c_str(), &a->sin_addr) != 1) return E2SARErrorInfo{E2SARErrorc::ParameterError, "bad IPv4 address " + ip};
+        sl = sizeof(sockaddr_in);
+    }
+    const int fd = socket(v6 ? AF_INET6 : AF_INET, SOCK_DGRAM, 0);
+    if (fd < 0) return E2SARErrorInfo{E2SARErrorc::SocketError, strerror(errno)};
+    // connect() on a UDP socket sends nothing; it makes the kernel pick the route
+    sockaddr_storage local{};
+    socklen_t ll = sizeof(local);
+    if (connect(fd, reinterpret_cast<sockaddr *>(&ss), sl) != 0 ||
+        getsockname(fd, reinterpret_cast<sockaddr *>(&local), &ll) != 0) {
+        const std::string err = strerror(errno);
+        close(fd);
+        return E2SARErrorInfo{E2SARErrorc::SocketError, "no route to " + ip + ": " + err};
+    }
+    ifaddrs *ifa = nullptr;
+    if (getifaddrs(&ifa) != 0) {
+        close(fd);
+        return E2SARErrorInfo{E2SARErrorc::SocketError, strerror(errno)};
+    }
+    std::string name;
+    for (ifaddrs *i = ifa; i && name.empty(); i = i->ifa_next) {
+        if (!i->ifa_addr || i->ifa_addr->sa_family != local.ss_family) continue;
+        if (v6) {
+            if (!memcmp(&reinterpret_cast<sockaddr_in6 *>(i->ifa_addr)->sin6_addr,
+                        &reinterpret_cast<sockaddr_in6 *>(&local)->sin6_addr, sizeof(in6_addr)))
+                name = i->ifa_name;
+        } else if (reinterpret_cast<sockaddr_in *>(i->ifa_addr)->sin_addr.s_addr ==
+                   reinterpret_cast<sockaddr_in *>(&local)->sin_addr.s_addr) {
+            name = i->ifa_name;
+        }
+    }
+    freeifaddrs(ifa);
+    if (name.empty()) {
+        close(fd);
+        return E2SARErrorInfo{E2SARErrorc::NotFound, "no interface holds the local address routed to " + ip};
+    }
+    ifreq ifr{};
+    strncpy(ifr.ifr_name, name.c_str(), IFNAMSIZ - 1);
+    const int rc = ioctl(fd, SIOCGIFMTU, &ifr);
+    close(fd);
+    if (rc != 0) return E2SARErrorInfo{E2SARErrorc::SocketError, std::string("SIOCGIFMTU: ") + strerror(errno)};
+    return std::make_tuple(name, (uint16_t)std::min(ifr.ifr_mtu, 65535));
+}
+
 }  // namespace NetUtil
 
 }  // namespace e2sar

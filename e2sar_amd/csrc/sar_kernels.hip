@@ -1293,7 +1293,36 @@ __global__ __launch_bounds__(kBlock) void zero_words_kernel(uint32_t *p, uint64_
         p[i] = 0u;
 }
 
+// Gather copy: blockIdx.y = span; 16-byte loads and stores when both ends are 16-byte
+// aligned (arena event buffers are 256-aligned; callers lay destinations out 64-aligned),
+// bytes otherwise and for the tail.
+__global__ __launch_bounds__(kBlock) void copy_spans_kernel(CopySpans cs)
+{
+    if (blockIdx.y >= cs.n) return;
+    const CopySpan sp = cs.s[blockIdx.y];
+    const uint8_t *src = reinterpret_cast<const uint8_t *>(sp.src);
+    uint8_t *dst = reinterpret_cast<uint8_t *>(sp.dst);
+    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+    uint64_t whole = 0;
+    if (((sp.src | sp.dst) & 15u) == 0) {
+        whole = sp.bytes & ~15ull;
+        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; 16 * i < whole; i += stride)
+            *reinterpret_cast<u32x4 *>(dst + 16 * i) = *reinterpret_cast<const u32x4 *>(src + 16 * i);
+    }
+    for (uint64_t b = whole + (uint64_t)blockIdx.x * kBlock + threadIdx.x; b < sp.bytes; b += stride) dst[b] = src[b];
+}
+
+hipError_t launch_copy_spans(const CopySpans &cs, uint64_t largest, hipStream_t stream)
+{
+    if (cs.n == 0 || largest == 0) return hipSuccess;
+    const uint64_t per = (uint64_t)kBlock * 16 * 4;             // 4 chunks per thread per block
+    const uint32_t bx = (uint32_t)std::min<uint64_t>(1024, (largest + per - 1) / per);
+    hipLaunchKernelGGL(copy_spans_kernel, dim3(bx, cs.n), dim3(kBlock), 0, stream, cs);
+    return hipGetLastError();
+}
+
 // ---------------------------------------------------------------------------------
+// GC / recycle// ---------------------------------------------------------------------------------
 // GC / recycle
 
 __global__ __launch_bounds__(kBlock) void reas_gc_kernel(ReasDev R, uint64_t now, uint64_t timeout)

@@ -142,6 +142,17 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
                               uint32_t n, uint64_t now, void *work, void *scratch, size_t scratchBytes,
                               hipStream_t stream);
 
+// Gather copy of up to kCopySpansPerLaunch spans (passed by value in the kernel arguments).
+constexpr uint32_t kCopySpansPerLaunch = 64;
+struct CopySpan {
+    uint64_t src, dst, bytes;
+};
+struct CopySpans {
+    CopySpan s[kCopySpansPerLaunch];
+    uint32_t n;
+};
+hipError_t launch_copy_spans(const CopySpans &cs, uint64_t largest, hipStream_t stream);
+
 // d_count (optional): the event count is read on the device; nEvents is then its bound
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,

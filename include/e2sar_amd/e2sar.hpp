@@ -129,6 +129,11 @@ const std::string get_Version();
 // e2sarNetUtil.hpp: the one helper the data-path tools use
 namespace NetUtil {
 result<std::string> getHostName() noexcept;
+// The interface the kernel routes `ip` through and its MTU (e2sarNetUtil.hpp:52,
+// e2sarNetUtil.cpp:77): a connected UDP socket selects the route, its local address names
+// the interface (getifaddrs), SIOCGIFMTU reads the MTU.  Replaces the reference's
+// RTM_GETROUTE netlink query with the same answer for routed destinations.
+result<std::tuple<std::string, uint16_t>> getInterfaceAndMTU(const std::string &ip) noexcept;
 }
 
 // Flag structs are declared at namespace scope so their default member initialisers
@@ -178,6 +183,9 @@ struct ReassemblerFlagsT {
     size_t arenaBytes{size_t(1) << 30};   // device event arena (x2 for compaction)
     uint32_t tableSlots{4096};
     int batchTimeout_us{200};             // flush a partial batch after this long
+    // the reference's arrival-order rules on the device (E2SAR_HIP_REAS_REFERENCE_ORDER):
+    // offset 0 always starts a new item, completion tested per fragment (cpp:361-427)
+    bool referenceOrder{false};
     static result<ReassemblerFlagsT> getFromINI(const std::string &iniFile) noexcept;
 };
 
@@ -264,6 +272,15 @@ public:
     const std::pair<int, int> get_recvPorts() const noexcept;
     int get_portRange() const noexcept;
     const std::string get_dataIP() const noexcept;
+    // device-path diagnostics (no reference counterpart): table / arena occupancy, error
+    // flags (bit0 table full, bit1 arena full, bit2 probe timeout) and how many times the
+    // table and arena were recycled or compacted
+    struct DeviceStats {
+        uint64_t tableUsed, arenaUsed, upkeeps;
+        int64_t inProgress;
+        uint32_t errorFlags;
+    };
+    const DeviceStats getDeviceStats() const noexcept;
     void stopThreads();
 
     struct Impl;

@@ -76,6 +76,27 @@ int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_
                            void *stream);
 int e2sar_hip_stream_sync(e2sar_hip_ctx *ctx, void *stream);
 
+/* stream ordering for callers without a HIP toolchain (the C++ facade pipelines its
+ * host->device copies beside the reassembly kernels with these): an event records the
+ * point a stream has reached; another stream can wait for it, the host can query or wait. */
+int e2sar_hip_event_create(e2sar_hip_ctx *ctx, void **out);
+int e2sar_hip_event_destroy(void *event);
+int e2sar_hip_event_record(e2sar_hip_ctx *ctx, void *event, void *stream);   /* NULL stream = context stream */
+int e2sar_hip_stream_wait_event(e2sar_hip_ctx *ctx, void *stream, void *event);
+int e2sar_hip_event_query(void *event);        /* 1 = reached, 0 = not yet, < 0 = error */
+int e2sar_hip_event_sync(void *event);
+
+/* Gather copy: n spans {src, dst, bytes}, device or pinned host memory on either side
+ * (pinned memory from e2sar_hip_host_alloc is device-accessible at the same address), in
+ * one kernel launch per 64 spans on `stream`.  This is how completed events leave the
+ * device arena in one batch instead of one memcpy per event. */
+typedef struct e2sar_hip_copy_span {
+    const void *src;
+    void *dst;
+    uint64_t bytes;
+} e2sar_hip_copy_span;
+int e2sar_hip_copy_spans(e2sar_hip_ctx *ctx, const e2sar_hip_copy_span *spans, uint32_t n, void *stream);
+
 /* ------------------------------------------------------------------ */
 /* geometry (e2sarHeaders.hpp:415-421, e2sarDPSegmenter.hpp:241, e2sarDPSegmenter.cpp:670) */
 

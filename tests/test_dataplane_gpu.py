@@ -489,3 +489,118 @@ def test_ipv6_loopback(E):
     for k, e in enumerate(evs):
         assert np.array_equal(got[100 + k], e)
     assert seg.getSendStats().msgCnt == sum(O.num_packets(e.nbytes, 1416) for e in evs)
+
+
+# ------------------------------- facade upkeep / reference order -----------------
+
+def _send_raw(port, datagrams):
+    s = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    s.setsockopt(socket.SOL_SOCKET, socket.SO_SNDBUF, 8 << 20)
+    for d in datagrams:
+        s.sendto(d, (DP, port))
+        time.sleep(0)
+    s.close()
+
+
+def _drain_events(reas, n, timeout=20.0):
+    got = {}
+    deadline = time.time() + timeout
+    while len(got) < n and time.time() < deadline:
+        r = reas.getEventBytes()
+        if r[0] < 0:
+            time.sleep(0.002)
+            continue
+        got[r[2]] = r[1]
+    return got
+
+
+def test_streaming_more_events_than_table_slots(E):
+    # 600 five-datagram events through a 64-slot table, each event's tail sent after the
+    # next event's head, so an event is always in progress: completed slots must be
+    # compacted away while events are in flight (a recycle never gets the chance), with no
+    # table exhaustion, no data errors and every event received intact
+    port = next_port()
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync=192.168.0.1:12345&data={DP}",
+                     E.EjfatURI.TokenType.instance)
+    f = E.DataPlane.Reassembler.ReassemblerFlags()
+    f.useCP = False
+    f.withLBHeader = True
+    f.rcvSocketBufSize = 8 << 20
+    f.arenaBytes = 64 << 20
+    f.tableSlots = 64
+    f.recvBatch = 64
+    f.recvStride = 128
+    f.batchTimeout_us = 100
+    reas = E.DataPlane.Reassembler(uri, E.IPAddress.from_string(DP), port, 1, f)
+    ok(reas.OpenAndStart())
+    mp = O.max_pld_len(80)
+    n_ev = 600
+    evs, frags = [], []
+    for k in range(n_ev):
+        ev = np.random.default_rng(9000 + k).integers(0, 256, 67, dtype=np.uint8)
+        pk, ln = O.segment_event(ev, 5000 + k, 7, 1, 2, 2, mp)
+        evs.append(ev.tobytes())
+        frags.append([pk[j, : int(ln[j])].tobytes() for j in range(len(ln))])
+    order = list(frags[0][:3])
+    for k in range(1, n_ev):
+        order += frags[k][:3] + frags[k - 1][3:]
+    order += frags[n_ev - 1][3:]
+    for i in range(0, len(order), 200):
+        _send_raw(port, order[i:i + 200])
+        time.sleep(0.005)
+    got = _drain_events(reas, n_ev)
+    st = reas.getStats()
+    ds = reas.getDeviceStats()
+    reas.stopThreads()
+    assert len(got) == n_ev, (len(got), st.dataErrCnt, ds.errorFlags, ds.tableUsed)
+    assert all(got[5000 + k] == evs[k] for k in range(n_ev))
+    assert st.dataErrCnt == 0 and st.eventSuccess == n_ev and ds.errorFlags == 0
+    assert ds.upkeeps > 0
+
+
+@pytest.mark.parametrize("reference_order", [False, True])
+def test_late_offset0_through_the_facade(E, reference_order):
+    # fragments 1, 0, 2, 3, 4 of one event: the reference replaces the item when offset 0
+    # arrives late (e2sarDPReassembler.cpp:361-369), so the event never completes and GC
+    # logs the new item lost with 4 fragments; the default device path completes it
+    port = next_port()
+    uri = E.EjfatURI(f"ejfat://useless@192.168.100.1:9875/lb/1?sync=192.168.0.1:12345&data={DP}",
+                     E.EjfatURI.TokenType.instance)
+    f = E.DataPlane.Reassembler.ReassemblerFlags()
+    f.useCP = False
+    f.withLBHeader = True
+    f.eventTimeout_ms = 200
+    f.referenceOrder = reference_order
+    f.arenaBytes = 16 << 20
+    reas = E.DataPlane.Reassembler(uri, E.IPAddress.from_string(DP), port, 1, f)
+    ok(reas.OpenAndStart())
+    mp = O.max_pld_len(80)
+    pk, ln = O.segment_event(np.frombuffer(SEND_STR, np.uint8), 77, 3, 5, 6, 2, mp)
+    for j in (1, 0, 2, 3, 4):
+        _send_raw(port, [pk[j, : int(ln[j])].tobytes()])
+        time.sleep(0.02)                       # one datagram per batch: arrival order kept
+    if reference_order:
+        deadline = time.time() + 5
+        lost = ()
+        while time.time() < deadline and lost == ():
+            time.sleep(0.05)
+            lost = reas.get_LostEvent()
+        assert lost == (77, 3, 4)
+        st = reas.getStats()
+        assert st.eventSuccess == 0 and st.reassemblyLoss == 1
+    else:
+        got = _drain_events(reas, 1, timeout=5)
+        assert got == {77: SEND_STR}
+    reas.stopThreads()
+
+
+def test_mtu_auto_detect_from_the_outgoing_interface(E):
+    # mtu 0: the MTU of the interface the data address routes through
+    # (e2sarDPSegmenter.cpp:56-110); loopback reports 65536, capped at the 9000-byte limit
+    # the device slot layout shares with the reference's override check (hpp:310-311)
+    port = next_port()
+    seg = make_seg(E, port, mtu=0)
+    assert seg.getIntf() == "lo"
+    assert seg.getMTU() == 9000 and seg.getMaxPldLen() == 9000 - 64
+    seg2 = make_seg(E, port, mtu=1500)
+    assert seg2.getIntf() == "lo" and seg2.getMTU() == 1500

@@ -5,10 +5,15 @@
 // to show that a program using e2sar::Segmenter / e2sar::Reassembler the way
 // e2sar_perf does runs on the gfx950 path.  Options are parsed by hand (no Boost here).
 //
-//   e2sar_perf -s -u URI --ip IP -l BYTES -n COUNT -m MTU --rate GBPS --sockets N
-//   e2sar_perf -r -u URI --ip IP --port P --threads N --duration S --timeout MS
+//   e2sar_perf -s -u URI --ip IP -l BYTES -n COUNT -e START -m MTU --rate GBPS --sockets N
+//              [--multiport] [--dpv6] [--smooth] [--realmalloc]
+//   e2sar_perf -r -u URI --ip IP --port P --threads N --deq N --duration S --timeout MS
+//              [--period MS] [-m MTU]
 //   e2sar_perf --loopback ...   both sides in one process over 127.0.0.1 (no LB in
 //                               between, so the receiver keeps the LB header: withLBHeader)
+// Receive slots are sized from -m (a datagram is at most MTU - 28 bytes over IPv4), so a
+// 1500-byte MTU does not move 9000-byte slots to the device; a larger datagram is
+// truncated and counted in dataErrCnt.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -26,14 +31,18 @@ using clk = std::chrono::steady_clock;
 
 namespace {
 
+std::atomic<size_t> sharedReceived{0};   // events received by all dequeue threads
+
 const std::string kHead = "[e2sar_perf event head]";
 const std::string kTail = "[e2sar_perf event tail]";
 
 struct Opts {
     bool send = false, recv = false, loopback = false, quiet = false;
+    bool multiport = false, dpv6 = false, smooth = false, realmalloc = false;
     std::string uri, ip = "127.0.0.1";
-    size_t length = 1 << 20, num = 10, threads = 1, sockets = 4;
-    uint16_t mtu = 1500, port = 10000, dataId = 4321, lbHdrVersion = 2;
+    size_t length = 1 << 20, num = 10, threads = 1, sockets = 4, deq = 1;
+    EventNum_t startEvent = 0;
+    uint16_t mtu = 1500, port = 10000, dataId = 4321, lbHdrVersion = 2, periodMs = 1000;
     uint32_t src = 1234;
     float rate = 1.0f;
     int duration = 0, timeoutMs = 500, bufsize = 3 << 20;
@@ -71,6 +80,13 @@ bool parse(int argc, char **argv, Opts &o)
         else if (a == "--timeout") o.timeoutMs = atoi(need("--timeout"));
         else if (a == "-b" || a == "--bufsize") o.bufsize = atoi(need("--bufsize"));
         else if (a == "-i" || a == "--ini") o.ini = need("--ini");
+        else if (a == "-e" || a == "--enum") o.startEvent = strtoull(need("--enum"), nullptr, 10);
+        else if (a == "--deq") o.deq = strtoull(need("--deq"), nullptr, 10);
+        else if (a == "-p" || a == "--period") o.periodMs = (uint16_t)atoi(need("--period"));
+        else if (a == "--multiport") o.multiport = true;
+        else if (a == "--dpv6") o.dpv6 = true;
+        else if (a == "--smooth") o.smooth = true;
+        else if (a == "--realmalloc") o.realmalloc = true;
         else {
             fprintf(stderr, "unknown option %s\n", a.c_str());
             return false;
@@ -80,6 +96,20 @@ bool parse(int argc, char **argv, Opts &o)
         fprintf(stderr, "exactly one of -s, -r, --loopback\n");
         return false;
     }
+    // the reference's conflicting_options (bin/e2sar_perf.cpp:440-460)
+    if (o.recv && (o.startEvent || o.smooth || o.multiport || o.realmalloc)) {
+        fprintf(stderr, "--enum, --smooth, --multiport, --realmalloc are sender options\n");
+        return false;
+    }
+    if (o.send && o.deq != 1) {
+        fprintf(stderr, "--deq is a receiver option\n");
+        return false;
+    }
+    if (o.rate < 0 && o.smooth) {
+        fprintf(stderr, "--smooth needs a positive --rate\n");
+        return false;
+    }
+    if (o.deq == 0) o.deq = 1;
     if (o.uri.empty())
         o.uri = "ejfat://token@127.0.0.1:18020/lb/1?data=" + o.ip + ":" + std::to_string(o.port);
     return true;
@@ -107,18 +137,32 @@ SendResult sendEvents(Segmenter &s, const Opts &o)
         fprintf(stderr, "openAndStart: %s\n", open.error().message().c_str());
         exit(1);
     }
+    // one event buffer reused for every event unless --realmalloc (bin/e2sar_perf.cpp:
+    // 148-170, 664-686); with one buffer nothing is freed by the callback
+    uint8_t *one = nullptr;
+    if (!o.realmalloc) {
+        one = static_cast<uint8_t *>(malloc(o.length));
+        memcpy(one, kHead.data(), kHead.size());
+        memcpy(one + o.length - kTail.size(), kTail.data(), kTail.size());
+    }
     const auto t0 = clk::now();
     size_t evt = 0;
     for (; evt < o.num; evt++) {
-        auto *buf = static_cast<uint8_t *>(malloc(o.length));
-        memcpy(buf, kHead.data(), kHead.size());
-        memcpy(buf + o.length - kTail.size(), kTail.data(), kTail.size());
+        uint8_t *buf = one;
+        if (!buf) {
+            buf = static_cast<uint8_t *>(malloc(o.length));
+            memcpy(buf, kHead.data(), kHead.size());
+            memcpy(buf + o.length - kTail.size(), kTail.data(), kTail.size());
+        }
+        // --enum is the first event number (the reference's loop passes evt itself, :175)
+        const EventNum_t en = o.startEvent + evt;
         for (;;) {
-            auto r = s.addToSendQueue(buf, o.length, evt, 0, 0, &freeBuffer, buf);
+            auto r = one ? s.addToSendQueue(buf, o.length, en, 0, 0, nullptr, nullptr)
+                         : s.addToSendQueue(buf, o.length, en, 0, 0, &freeBuffer, buf);
             if (!r.has_error()) break;
             if (r.error().code() != E2SARErrorc::MemoryError) {
                 fprintf(stderr, "addToSendQueue: %s\n", r.error().message().c_str());
-                free(buf);
+                if (!one) free(buf);
                 break;
             }
             std::this_thread::yield();   // queue full, try again (e2sar_perf :176-188)
@@ -130,6 +174,10 @@ SendResult sendEvents(Segmenter &s, const Opts &o)
         std::this_thread::sleep_for(std::chrono::microseconds(100));
     }
     res.seconds = std::chrono::duration<double>(clk::now() - t0).count();
+    if (one) {
+        s.stopThreads();            // every datagram of the shared buffer has left
+        free(one);
+    }
     auto st = s.getSendStats();
     res.events = evt;
     res.frames = st.msgCnt;
@@ -146,6 +194,7 @@ struct RecvResult {
     double firstToLast = 0;
 };
 
+// One dequeue thread (the reference starts --deq of them, bin/e2sar_perf.cpp:763-769).
 RecvResult recvEvents(Reassembler &r, const Opts &o, size_t stopAfter, std::atomic<bool> &stop)
 {
     RecvResult res;
@@ -171,10 +220,45 @@ RecvResult recvEvents(Reassembler &r, const Opts &o, size_t stopAfter, std::atom
             memcmp(buf + bytes - kTail.size(), kTail.data(), kTail.size()))
             res.mangled++;
         delete[] buf;   // ownership passes to the caller (e2sar_perf :299)
-        if (stopAfter && res.received >= stopAfter) break;
+        if (stopAfter && sharedReceived.fetch_add(1) + 1 >= stopAfter) stop.store(true);
     }
     res.firstToLast = std::chrono::duration<double>(last - first).count();
     return res;
+}
+
+// --deq dequeue threads, results summed
+RecvResult recvEventsMT(Reassembler &r, const Opts &o, size_t stopAfter, std::atomic<bool> &stop)
+{
+    sharedReceived = 0;
+    std::vector<RecvResult> rs(o.deq);
+    std::vector<std::thread> ts;
+    for (size_t i = 0; i < o.deq; i++) ts.emplace_back([&, i] { rs[i] = recvEvents(r, o, stopAfter, stop); });
+    // the receive-side reporting thread (bin/e2sar_perf.cpp:306-355), every --period ms
+    std::thread rep;
+    if (!o.quiet && o.recv)
+        rep = std::thread([&] {
+            while (!stop.load()) {
+                for (int k = 0; k < o.periodMs / 10 && !stop.load(); k++)
+                    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+                auto st = r.getStats();
+                printf("Stats: eventSuccess=%llu enqueueLoss=%llu reassemblyLoss=%llu totalPackets=%zu\n",
+                       (unsigned long long)st.eventSuccess, (unsigned long long)st.enqueueLoss,
+                       (unsigned long long)st.reassemblyLoss, st.totalPackets);
+                fflush(stdout);
+            }
+        });
+    for (auto &t : ts) t.join();
+    stop.store(true);
+    if (rep.joinable()) rep.join();
+    RecvResult all;
+    for (const auto &x : rs) {
+        all.received += x.received;
+        all.mangled += x.mangled;
+        all.errors += x.errors;
+        all.bytes += x.bytes;
+        all.firstToLast = std::max(all.firstToLast, x.firstToLast);
+    }
+    return all;
 }
 
 void printRecv(Reassembler &r, const RecvResult &rr)
@@ -228,10 +312,14 @@ int main(int argc, char **argv)
         sflags.numSendSockets = o.sockets;
         sflags.rateGbps = o.rate;
         sflags.lbHdrVersion = (uint8_t)o.lbHdrVersion;
+        sflags.multiPort = o.multiport;
+        sflags.smooth = o.smooth;
+        sflags.dpV6 = o.dpv6;
         rflags.useCP = false;
         rflags.withLBHeader = true;       // back to back: nobody strips the LB header
         rflags.eventTimeout_ms = o.timeoutMs;
         rflags.rcvSocketBufSize = o.bufsize;
+        rflags.recvStride = ((size_t)o.mtu - 28 + 15) & ~(size_t)15;
     }
 
     try {
@@ -248,7 +336,7 @@ int main(int argc, char **argv)
         if (open.has_error()) return fprintf(stderr, "openAndStart: %s\n", open.error().message().c_str()), 1;
         printf("Receiving on %s ports %d-%d\n", o.ip.c_str(), r.get_recvPorts().first, r.get_recvPorts().second);
         if (o.recv) {
-            auto rr = recvEvents(r, o, 0, stop);
+            auto rr = recvEventsMT(r, o, 0, stop);
             printRecv(r, rr);
             r.stopThreads();
             return 0;
@@ -257,7 +345,7 @@ int main(int argc, char **argv)
         // addToSendQueue to the last validated event
         RecvResult rr;
         const auto t0 = clk::now();
-        std::thread rt([&] { rr = recvEvents(r, o, o.num, stop); });
+        std::thread rt([&] { rr = recvEventsMT(r, o, o.num, stop); });
         Segmenter s(uri, o.dataId, o.src, sflags);
         printf("Event size is %zu bytes, sending %zu events, MTU %u\n", o.length, o.num, s.getMTU());
         sendEvents(s, o);

@@ -73,6 +73,9 @@ def parse(argv=None):
     ap.add_argument("--cold-steps", type=int, default=10,
                     help="steps of the cold receive-only leg (0 = skip): reassembly of datagrams that were "
                          "written long before and are read back from HBM")
+    ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="pipelined",
+                    help="launch form of the cold leg (split: classify + scatter launches, timed apart; "
+                         "pipelined: classify(0), then scatter(b) beside classify(b+1) in one launch)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -556,12 +559,28 @@ def main():
         cbufs = [seg.alloc_packets(p.total_packets) for p in plans]
         for p, (pk, ln) in zip(plans, cbufs):
             seg.segment(p, pk, ln)
+        cwork = [R.alloc_work(max_batch_pk) for _ in range(2)] if args.cold_reas != "fused" else None
         torch.cuda.synchronize()
 
         def cstep():
             R.recycle(force=True)
+            if args.cold_reas == "pipelined":
+                p0, (pk0, ln0) = plans[0], cbufs[0]
+                timed("reas_classify_kernel", R.classify, pk0, stride, ln0, p0.total_packets, cwork[0])
+                for k, (p, (pk, ln)) in enumerate(zip(plans, cbufs)):
+                    if k + 1 < len(plans):
+                        q, (qpk, qln) = plans[k + 1], cbufs[k + 1]
+                        timed("reas_scatter_classify_kernel", R.scatter_classify, stride, pk, p.total_packets,
+                              cwork[k % 2], qpk, qln, q.total_packets, cwork[(k + 1) % 2])
+                    else:
+                        timed("reas_scatter_kernel", R.scatter, pk, stride, p.total_packets, cwork[k % 2])
+                return
             for p, (pk, ln) in zip(plans, cbufs):
-                timed("reas_kernel", R.reassemble, pk, stride, ln, p.total_packets)
+                if cwork is None:
+                    timed("reas_kernel", R.reassemble, pk, stride, ln, p.total_packets)
+                else:
+                    timed("reas_classify_kernel", R.classify, pk, stride, ln, p.total_packets, cwork[0])
+                    timed("reas_scatter_kernel", R.scatter, pk, stride, p.total_packets, cwork[0])
 
         cstep()
         torch.cuda.synchronize()
@@ -570,17 +589,24 @@ def main():
         ck = max(G, args.cold_steps // G * G)
         cel = run_timed(cstep, cgraph, ck)
         cper = kernel_times(cstep, args.roofline_steps)
-        c_ms = sum(cper["reas_kernel"]) / len(cper["reas_kernel"])
+        ckern = {"fused": "reas_kernel", "split": "reas_scatter_kernel",
+                 "pipelined": "reas_scatter_classify_kernel"}[args.cold_reas]
+        c_ms = sum(cper[ckern]) / len(cper[ckern])
         c_ach = launch_bytes / (c_ms * 1e-3) / 1e9
         cold = {
-            "what": "reas_kernel alone on datagrams written long before (one buffer per batch, "
-                    f"{step_pk * stride / 1e9:.2f} GB per step, read back from HBM); value = payload "
+            "what": f"reassembly alone ({args.cold_reas} form) on datagrams written long before (one buffer "
+                    f"per batch, {step_pk * stride / 1e9:.2f} GB per step, read back from HBM); value = payload "
                     "reassembled per second",
+            "form": {"fused": "reas_kernel per batch",
+                     "split": "reas_classify_kernel + reas_scatter_kernel per batch",
+                     "pipelined": "reas_classify_kernel(0), then reas_scatter_classify_kernel: scatter(b) "
+                                  "beside classify(b+1)"}[args.cold_reas],
             "value": round(E * B * world * ck / cel / 2**30, 3), "unit": "GiB/s", "steps": ck,
             "ms_per_step": round(cel / ck * 1e3, 4), "verified": cver,
-            "roofline": {"bound": "hbm", "kernel": "reas_kernel", "achieved": round(c_ach, 1),
+            "roofline": {"bound": "hbm", "kernel": ckern, "achieved": round(c_ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(c_ach / HBM_PEAK_GBS, 4),
-                         "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(launch_bytes)},
+                         "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(launch_bytes),
+                         "all_launch_ms": {k: round(sum(v) / len(v), 5) for k, v in cper.items()}},
         }
         del cbufs
 

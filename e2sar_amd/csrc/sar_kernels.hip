@@ -45,6 +45,12 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_SEG_U
 #define E2SAR_SEG_U 4               // 16-byte output chunks per thread of seg_kernel
 #endif
+#ifndef E2SAR_REAS_PIPE
+#define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
+#endif
+#ifndef E2SAR_SCATTER_CHUNKS_PER_BLOCK
+#define E2SAR_SCATTER_CHUNKS_PER_BLOCK 1024u
+#endif
 #ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
 #define E2SAR_REAS_CHUNKS_PER_BLOCK 9216u
 #endif
@@ -924,6 +930,9 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
         }
     };
     u32x4 x[U];
+#if E2SAR_REAS_PIPE
+    u32x4 y[U];
+#endif
     issue(0u, x);                      // round 0 is in flight while wave 0 classifies
 
     unsigned long long old = 0;
@@ -944,11 +953,28 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     lds_barrier();
     TRACE_AT(0, 2, trace_hwid());
 
+#if E2SAR_REAS_PIPE
+    // software pipeline: the loads of round r+1 are issued before the stores of round r.
+    // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
+    // a store can only be waited for together with that store's write acknowledgement;
+    // issued before it, round r+1's data is waited for while round r's stores drain.
+    constexpr uint32_t RS = (uint32_t)(kBlock * U);
+    if (RS < nch) issue(RS, y);
+    store(0u, x);
+    for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
+        if (r0 + RS < nch) issue(r0 + RS, x);
+        store(r0, y);
+        if (r0 + RS >= nch) break;
+        if (r0 + 2 * RS < nch) issue(r0 + 2 * RS, y);
+        store(r0 + RS, x);
+    }
+#else
     store(0u, x);
     for (uint32_t r0 = (uint32_t)(kBlock * U); r0 < nch; r0 += (uint32_t)(kBlock * U)) {
         issue(r0, x);
         store(r0, x);
     }
+#endif
 
     if (w0 && L.tail[lane]) {
         Classified cl;
@@ -1538,10 +1564,14 @@ static uint32_t occupancy_lds(const char *var)
 
 static uint32_t scatter_group_size(uint32_t stride)
 {
-    // datagrams per scatter workgroup: at most E2SAR_REAS_CHUNKS_PER_BLOCK 16-byte chunks, <= 64
+    // datagrams per scatter workgroup: at most E2SAR_SCATTER_CHUNKS_PER_BLOCK 16-byte chunks
+    // (one round of 256 threads x 4), <= 64.  The scatter needs no table round trip, so it
+    // streams best in one-round workgroups, like seg_kernel: at 205 x 1 MiB, MTU 1500, a
+    // batch read back cold takes 81.5 us with 1K-chunk groups against 100.3 us with the
+    // fused kernel's 9K budget (89.5 us at 2K); hot, 68.7 us.
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > E2SAR_REAS_CHUNKS_PER_BLOCK) G >>= 1;
+    while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK) G >>= 1;
     return G;
 }
 

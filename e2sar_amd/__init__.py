@@ -6,7 +6,10 @@ include/e2sar_hip.h.  Submodules:
 
   _capi      ctypes binding of the C ABI (loads e2sar_amd/lib/libe2sar_hip.so)
   sar        device-level batch API (DeviceSegmenter / DeviceReassembler)
-  headers    wire-format classes mirroring the reference pybind header bindings
+  dist       multi-GPU routing (PacketRouter) and the all-to-all-v exchange
+  e2sar_py   pybind module with the reference's e2sar_py names (DataPlane.Segmenter /
+             Reassembler, header classes REHdr / LBHdrV2 / LBHdrV3 / SyncHdr, EjfatURI),
+             built from csrc/host/py_e2sar.cpp over the C++ facade
 """
 
 __version__ = "0.1.0"

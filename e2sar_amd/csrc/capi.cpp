@@ -356,10 +356,10 @@ int e2sar_hip_segment_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_eve
     if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
         return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
     if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
-    const bool a4 = eventsDwordAligned && (maxPldLen % 4u == 0);
+    (void)eventsDwordAligned;        // a hint only: the kernel checks every event's address itself
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    hipError_t e = launch_segment(d_events, nEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen, a4,
+    hipError_t e = launch_segment(d_events, nEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen,
                                   d_packets, stride, d_lens, s);
     if (e != hipSuccess) return hip_fail(e, "seg_kernel launch");
     return E2SAR_HIP_OK;
@@ -380,7 +380,7 @@ int e2sar_hip_segment_batch_dev(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
     hipError_t e = launch_segment(d_events, maxEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen,
-                                  maxPldLen % 4u == 0, d_packets, stride, d_lens, s, d_counts);
+                                  d_packets, stride, d_lens, s, d_counts);
     if (e != hipSuccess) return hip_fail(e, "seg_kernel launch");
     return E2SAR_HIP_OK;
 }

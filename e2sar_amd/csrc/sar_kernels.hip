@@ -232,7 +232,9 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 // in flight together.
 // dCount (optional): the number of events is read on the device (the relay form, whose
 // event table is built by relay_plan_kernel); blocks of events past it exit.
-template <bool A4, int U>
+// The dword fast path (16-byte loads at dword alignment) is chosen per event from the
+// event's own address and maxPld: a block handles one event, so the choice is uniform.
+template <int U>
 __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                      uint32_t blocksPerEvent, int lbVersion,
                                                      uint32_t maxPld, uint8_t *__restrict__ pkts,
@@ -244,6 +246,7 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
     const uint32_t bx = blockIdx.x - e * blocksPerEvent;
     if (dCount && e >= *dCount) return;
     const e2sar_hip_seg_event ev = events[e];
+    const bool A4 = (((uintptr_t)ev.data | maxPld) & 3u) == 0u;
     const uint32_t bytes = ev.bytes;
     const uint32_t npk = (bytes + maxPld - 1u) / maxPld;
     const uint32_t spc = stride >> 4;
@@ -1462,7 +1465,7 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
 
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
-                          bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
+                          uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream, const uint32_t *d_count)
 {
     constexpr int U = E2SAR_SEG_U;
@@ -1472,12 +1475,8 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     const uint32_t bpe = cdiv(chunks, (uint64_t)kBlock * U);
     const uint64_t grid = (uint64_t)bpe * nEvents;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    if (aligned4)
-        hipLaunchKernelGGL((seg_kernel<true, U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream,
-                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens, d_count);
-    else
-        hipLaunchKernelGGL((seg_kernel<false, U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream,
-                           d_events, bpe, lbVersion, maxPld, pkts, stride, lens, d_count);
+    hipLaunchKernelGGL((seg_kernel<U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
+                       maxPld, pkts, stride, lens, d_count);
     return hipGetLastError();
 }
 

@@ -156,7 +156,7 @@ hipError_t launch_copy_spans(const CopySpans &cs, uint64_t largest, hipStream_t 
 // d_count (optional): the event count is read on the device; nEvents is then its bound
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
-                          bool aligned4, uint8_t *pkts, uint32_t stride, uint32_t *lens,
+                          uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream, const uint32_t *d_count = nullptr);
 hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvents, uint32_t maxPld,
                              uint64_t lbTick, uint32_t entropyBase, e2sar_hip_seg_event *d_events,

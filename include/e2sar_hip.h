@@ -126,8 +126,10 @@ typedef struct e2sar_hip_seg_event {
 } e2sar_hip_seg_event;
 
 /* Host-side plan over a host copy of the event table: fills pktBase (exclusive prefix
- * of ceil(bytes/maxPldLen)), returns the batch packet count and the largest per-event
- * packet count.  Also reports whether every event is dword-aligned (fast path). */
+ * of ceil(bytes/maxPldLen)) and writes the batch's packet count and the largest per-event
+ * packet count to *totalPackets and *maxPacketsPerEvent (either may be NULL).  Returns a
+ * status: 0, or E2SAR_HIP_ERR_PARAMETER (NULL table, maxPldLen 0) / OUT_OF_RANGE (more
+ * than 2^32 - 1 packets). */
 int e2sar_hip_seg_plan(e2sar_hip_seg_event *events, uint32_t nEvents, size_t maxPldLen,
                        uint32_t *totalPackets, uint32_t *maxPacketsPerEvent);
 
@@ -135,8 +137,10 @@ int e2sar_hip_seg_plan(e2sar_hip_seg_event *events, uint32_t nEvents, size_t max
  * datagrams [16-byte LB][20-byte RE][payload] at d_packets + p*stride, p = pktBase+k.
  * d_lens[p] (optional) receives the datagram length 36 + payload.  lbHdrVersion 3
  * selects LBHdrV3, any other value LBHdrV2 (e2sarHeaders.hpp:287-297).
- * maxPacketsPerEvent: an upper bound (from seg_plan).  Asynchronous on `stream`
- * (NULL = the context stream). */
+ * maxPacketsPerEvent: an upper bound (from seg_plan).  eventsDwordAligned is a hint kept
+ * for ABI compatibility: the kernel takes its 16-byte dword-aligned fast path for every
+ * event whose address and maxPldLen are multiples of 4 and a byte path for the others,
+ * checking each event itself.  Asynchronous on `stream` (NULL = the context stream). */
 int e2sar_hip_segment_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events,
                             uint32_t nEvents, uint32_t maxPacketsPerEvent,
                             int lbHdrVersion, uint32_t maxPldLen, int eventsDwordAligned,

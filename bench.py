@@ -122,8 +122,8 @@ def host_cpu_info() -> dict:
 
 def cpu_baseline(args, budget_s: float):
     """The oracle (plain-C restatement of _send + recv body) on the host cores, on a bounded
-    sample of the same workload: each thread segments + reassembles its own 16 events of
-    event-bytes repeatedly.  Timed on 1 thread and on T threads, budget_s each; the
+    sample of the same workload: each thread segments + reassembles the sample's events
+    (64 x 1 MiB by default) repeatedly.  Timed on 1 thread and on T threads, budget_s each; the
     T-thread rate is the reported baseline.  T = the CPUs this process may use, capped at
     16: the GPU box allots 16 host CPUs per GPU (OMP_NUM_THREADS=16 there) although nproc
     shows the whole machine.  ctypes releases the GIL around every C call."""
@@ -135,7 +135,12 @@ def cpu_baseline(args, budget_s: float):
     import sar_inputs as S
 
     B = args.event_bytes
-    n_ev = max(1, min(16, (256 << 20) // B))
+    # events in the sample (E2SAR_CPU_EVENTS overrides): 64 MiB of events, more than a
+    # CCD's 32 MB L3, so one thread streams them from DRAM as 16 threads do (and as the GPU
+    # workload's 1 GiB does).  A 4-16 MiB sample runs one thread from its L3 at ~1.7x the
+    # DRAM rate, which is why an earlier 16-event sample showed 16 threads at only 1.3-2.6x
+    # one (tools/cpu_baseline_sweep.sh)
+    n_ev = int(os.environ.get("E2SAR_CPU_EVENTS", 0)) or max(1, min(64, (64 << 20) // B))
     mp = O.max_pld_len(args.mtu)
     stride = (36 + mp + 15) // 16 * 16
     npk = O.num_packets(B, mp)

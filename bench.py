@@ -61,10 +61,13 @@ def parse(argv=None):
                     help="steps captured in one HIP graph (0: the largest of 4, 2, 1 that divides --steps); "
                          "the timed region still runs exactly --steps steps")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
-    ap.add_argument("--reas", choices=["fused", "split", "pipelined"], default="fused",
+    ap.add_argument("--reas", choices=["fused", "split", "pipelined", "chained"], default="fused",
                     help="fused: one reassemble_batch launch per batch; split: classify + scatter launches "
                          "in line; pipelined: one launch scatters batch b while other workgroups classify "
-                         "batch b+1 (two datagram buffers, one stream)")
+                         "batch b+1 (two datagram buffers, one stream); chained: segmentation and "
+                         "reassembly of a batch in one launch (segment_reassemble_batch)")
+    ap.add_argument("--chain-batches", type=int, default=1,
+                    help="chained form: batches per launch (1-8; each batch its own datagram buffer)")
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
@@ -73,6 +76,10 @@ def parse(argv=None):
     ap.add_argument("--cold-steps", type=int, default=10,
                     help="steps of the cold receive-only leg (0 = skip): reassembly of datagrams that were "
                          "written long before and are read back from HBM")
+    ap.add_argument("--cold-batch-events", type=int, default=0,
+                    help="events per reassembly launch in the cold leg (0 = --batch-events); the cold leg "
+                         "does not depend on the Infinity Cache holding a batch, so larger launches only "
+                         "amortise a launch's head and tail")
     ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="pipelined",
                     help="launch form of the cold leg (split: classify + scatter launches, timed apart; "
                          "pipelined: classify(0), then scatter(b) beside classify(b+1) in one launch)")
@@ -264,16 +271,23 @@ def main():
         evnum = lambda i: i * world + rank      # every local event is owned here: eventNum % world == rank
     else:
         evnum = lambda i: rank * E + i          # owners spread over all ranks: datagrams must be exchanged
-    plans = []
-    for b0 in range(0, E, args.batch_events):
-        idx = range(b0, min(E, b0 + args.batch_events))
-        plans.append(seg.plan([(src[i].data_ptr(), B, evnum(i), 4321, 1 + (evnum(i) * 0x9E37) % 65535,
-                                (1 << 48) + evnum(i)) for i in idx]))
+    def make_plans(batch):
+        out = []
+        for b0 in range(0, E, batch):
+            idx = range(b0, min(E, b0 + batch))
+            out.append(seg.plan([(src[i].data_ptr(), B, evnum(i), 4321, 1 + (evnum(i) * 0x9E37) % 65535,
+                                  (1 << 48) + evnum(i)) for i in idx]))
+        return out
+
+    plans = make_plans(args.batch_events)
     max_batch_pk = max(p.total_packets for p in plans)
     step_pk = sum(p.total_packets for p in plans)
-    if args.reas == "pipelined" and args.overlap:
+    if args.reas in ("pipelined", "chained") and args.overlap:
         args.overlap = False                    # the pipeline is its own overlap
     nbuf = 2 if (args.overlap or args.reas == "pipelined") else 1
+    if args.reas == "chained":
+        args.chain_batches = max(1, min(8, args.chain_batches))
+        nbuf = min(args.chain_batches, len(plans))
     table = 1
     while table < args.table_factor * E:
         table <<= 1
@@ -302,7 +316,7 @@ def main():
         bufs = []
     else:
         bufs = [seg.alloc_packets(max_batch_pk) for _ in range(nbuf)]
-    works = [R.alloc_work(max_batch_pk) for _ in range(nbuf)] if args.reas != "fused" else None
+    works = [R.alloc_work(max_batch_pk) for _ in range(nbuf)] if args.reas in ("split", "pipelined") else None
     torch.cuda.synchronize()
 
     timing = []          # (kernel, start event, end event) while the roofline pass runs
@@ -368,6 +382,13 @@ def main():
                           works[k % 2], npk_, nln_, q.total_packets, works[(k + 1) % 2])
                 else:
                     timed("reas_scatter_kernel", R.scatter, pk, stride, p.total_packets, works[k % 2])
+            return
+        if args.reas == "chained":
+            K = args.chain_batches
+            for c0 in range(0, len(plans), K):
+                chunk = plans[c0:c0 + K]
+                timed("segreas_kernel", seg.segment_reassemble_batches, chunk,
+                      [bufs[(c0 + j) % nbuf] for j in range(len(chunk))], R)
             return
         if not args.overlap:
             pk, ln = bufs[0]
@@ -523,7 +544,7 @@ def main():
     #   record written per datagram -- is left out, so its rate is understated by ~1 %)
     launch_bytes = per_launch_events * (2 * B + 36 * npk)
     bw_kernels = [k for k in avg if k in ("seg_kernel", "reas_kernel", "reas_scatter_kernel",
-                                          "reas_scatter_classify_kernel")]
+                                          "reas_scatter_classify_kernel", "segreas_kernel")]
     dom = max(bw_kernels, key=lambda k: sum(per[k]))      # most time in the step
     dom_ms = avg[dom]
     if spread and dom == "reas_kernel":
@@ -531,6 +552,8 @@ def main():
         # datagrams (the last one fewer): average algorithmic bytes per launch
         owned = sum(1 for r in range(world) for i in range(E) if (r * E + i) % world == rank)
         launch_bytes = owned * (2 * B + 36 * npk) / (len(per[dom]) / max(1, args.roofline_steps))
+    if dom == "segreas_kernel":
+        launch_bytes *= 2                       # both stages' bytes in one launch: 4B + 72N per event
     achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
 
     # HBM traffic per launch of the dominant kernel, from the committed rocprofv3 PMC passes
@@ -561,26 +584,29 @@ def main():
     # Infinity Cache, so each launch reads its batch back from HBM) ----
     cold = None
     if args.cold_steps > 0 and not spread:
-        cbufs = [seg.alloc_packets(p.total_packets) for p in plans]
-        for p, (pk, ln) in zip(plans, cbufs):
+        cb = args.cold_batch_events or args.batch_events
+        cplans = plans if cb == args.batch_events else make_plans(cb)
+        cbufs = [seg.alloc_packets(p.total_packets) for p in cplans]
+        for p, (pk, ln) in zip(cplans, cbufs):
             seg.segment(p, pk, ln)
-        cwork = [R.alloc_work(max_batch_pk) for _ in range(2)] if args.cold_reas != "fused" else None
+        cmax_pk = max(p.total_packets for p in cplans)
+        cwork = [R.alloc_work(cmax_pk) for _ in range(2)] if args.cold_reas != "fused" else None
         torch.cuda.synchronize()
 
         def cstep():
             R.recycle(force=True)
             if args.cold_reas == "pipelined":
-                p0, (pk0, ln0) = plans[0], cbufs[0]
+                p0, (pk0, ln0) = cplans[0], cbufs[0]
                 timed("reas_classify_kernel", R.classify, pk0, stride, ln0, p0.total_packets, cwork[0])
-                for k, (p, (pk, ln)) in enumerate(zip(plans, cbufs)):
-                    if k + 1 < len(plans):
-                        q, (qpk, qln) = plans[k + 1], cbufs[k + 1]
+                for k, (p, (pk, ln)) in enumerate(zip(cplans, cbufs)):
+                    if k + 1 < len(cplans):
+                        q, (qpk, qln) = cplans[k + 1], cbufs[k + 1]
                         timed("reas_scatter_classify_kernel", R.scatter_classify, stride, pk, p.total_packets,
                               cwork[k % 2], qpk, qln, q.total_packets, cwork[(k + 1) % 2])
                     else:
                         timed("reas_scatter_kernel", R.scatter, pk, stride, p.total_packets, cwork[k % 2])
                 return
-            for p, (pk, ln) in zip(plans, cbufs):
+            for p, (pk, ln) in zip(cplans, cbufs):
                 if cwork is None:
                     timed("reas_kernel", R.reassemble, pk, stride, ln, p.total_packets)
                 else:
@@ -596,12 +622,20 @@ def main():
         cper = kernel_times(cstep, args.roofline_steps)
         ckern = {"fused": "reas_kernel", "split": "reas_scatter_kernel",
                  "pipelined": "reas_scatter_classify_kernel"}[args.cold_reas]
+        if ckern not in cper:                   # pipelined form with one batch: classify + scatter
+            ckern = "reas_scatter_kernel"
         c_ms = sum(cper[ckern]) / len(cper[ckern])
-        c_ach = launch_bytes / (c_ms * 1e-3) / 1e9
+        # per launch of ckern: the batches it scatters (the last batch's scatter-only launch
+        # is not ckern in the pipelined form)
+        c_ev = [p.n_events for p in cplans]
+        c_ev = c_ev[:-1] if ckern == "reas_scatter_classify_kernel" else c_ev
+        c_bytes = sum(c_ev) / len(c_ev) * (2 * B + 36 * npk)
+        c_ach = c_bytes / (c_ms * 1e-3) / 1e9
         cold = {
             "what": f"reassembly alone ({args.cold_reas} form) on datagrams written long before (one buffer "
                     f"per batch, {step_pk * stride / 1e9:.2f} GB per step, read back from HBM); value = payload "
                     "reassembled per second",
+            "batch_events": cb,
             "form": {"fused": "reas_kernel per batch",
                      "split": "reas_classify_kernel + reas_scatter_kernel per batch",
                      "pipelined": "reas_classify_kernel(0), then reas_scatter_classify_kernel: scatter(b) "
@@ -610,7 +644,7 @@ def main():
             "ms_per_step": round(cel / ck * 1e3, 4), "verified": cver,
             "roofline": {"bound": "hbm", "kernel": ckern, "achieved": round(c_ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(c_ach / HBM_PEAK_GBS, 4),
-                         "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(launch_bytes),
+                         "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(c_bytes),
                          "all_launch_ms": {k: round(sum(v) / len(v), 5) for k, v in cper.items()}},
         }
         del cbufs
@@ -648,7 +682,9 @@ def main():
                 "reassembly": {"fused": "reas_kernel per batch",
                                "split": "reas_classify_kernel + reas_scatter_kernel per batch",
                                "pipelined": "reas_scatter_classify_kernel: scatter(b) beside classify(b+1), "
-                                            "2 datagram buffers"}[args.reas],
+                                            "2 datagram buffers",
+                               "chained": "segreas_kernel per batch: seg blocks then reassembly groups in one "
+                                          "launch, per-group ready counters"}[args.reas],
                 "landing": args.landing,
                 "payload": args.payload,
                 "verified_roundtrip": verified,

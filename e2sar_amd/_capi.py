@@ -40,6 +40,18 @@ class SegEvent(C.Structure):
     ]
 
 
+class SegReasBatch(C.Structure):
+    _fields_ = [
+        ("d_events", C.c_uint64),
+        ("d_packets", C.c_uint64),
+        ("d_lens", C.c_uint64),
+        ("nEvents", C.c_uint32),
+        ("maxPacketsPerEvent", C.c_uint32),
+        ("nPackets", C.c_uint32),
+        ("reserved", C.c_uint32),
+    ]
+
+
 class ReasConfig(C.Structure):
     _fields_ = [
         ("withLBHeader", C.c_int),
@@ -142,6 +154,8 @@ SIGNATURES = {
     "e2sar_hip_seg_plan": (i, [C.POINTER(SegEvent), u32, sz, C.POINTER(u32), C.POINTER(u32)]),
     "e2sar_hip_segment_batch": (i, [vp, vp, u32, u32, i, u32, i, vp, u32, vp, vp]),
     "e2sar_hip_segment_batch_dev": (i, [vp, vp, vp, u32, u32, i, u32, vp, u32, vp, vp]),
+    "e2sar_hip_segment_reassemble_batch": (i, [vp, vp, u32, u32, u32, i, u32, vp, u32, vp, vp, u64, vp]),
+    "e2sar_hip_segment_reassemble_batches": (i, [vp, vp, u32, i, u32, u32, vp, u64, vp]),
     "e2sar_hip_relay_plan": (i, [vp, u32, u32, sz, u64, C.c_uint16, vp, vp, vp]),
     "e2sar_hip_reas_create": (i, [vp, C.POINTER(ReasConfig), C.POINTER(vp)]),
     "e2sar_hip_reas_destroy": (None, [vp]),

@@ -60,6 +60,9 @@ struct e2sar_hip_reas {
     size_t roScratchBytes = 0;
     void *roWork = nullptr;
     size_t roWorkBytes = 0;
+    // chained segment -> reassemble form: one ready counter per reassembly group
+    void *tiles = nullptr;
+    size_t tilesBytes = 0;
     std::mutex mu;
 };
 
@@ -90,6 +93,7 @@ static void reas_release(e2sar_hip_reas *r)
 {
     if (r->roScratch) (void)hipFree(r->roScratch);
     if (r->roWork) (void)hipFree(r->roWork);
+    if (r->tiles) (void)hipFree(r->tiles);
     if (r->altSlots) (void)hipFree(r->altSlots);
     if (r->alt.arena && r->alt.arena != r->dev.arena) (void)hipFree(r->alt.arena);
     if (r->dev.arena) (void)hipFree(r->dev.arena);
@@ -476,6 +480,7 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     (void)hipFree(r->stateMem);
     if (r->roScratch) (void)hipFree(r->roScratch);
     if (r->roWork) (void)hipFree(r->roWork);
+    if (r->tiles) (void)hipFree(r->tiles);
     delete r;
 }
 
@@ -520,6 +525,69 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;
+}
+
+static int segreas(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches, uint32_t nBatches, int lbHdrVersion,
+                   uint32_t maxPldLen, uint32_t stride, e2sar_hip_reas *r, uint64_t now_ms, void *stream)
+{
+    if (!ctx || !r || (!batches && nBatches)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    if (nBatches > kChainMaxBatches) return fail(E2SAR_HIP_ERR_PARAMETER, "more than 8 batches per launch");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    if (maxPldLen > 65535u) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen above a UDP datagram");
+    if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
+    if (!r->cfg.withLBHeader) return fail(E2SAR_HIP_ERR_PARAMETER, "the chained form emits LB headers: withLBHeader required");
+    if (ref_order(r)) return fail(E2SAR_HIP_ERR_PARAMETER, "the chained form is order-insensitive (no REFERENCE_ORDER)");
+    ChainBatches cb{};
+    uint64_t words = 0;
+    for (uint32_t b = 0; b < nBatches; b++) {
+        const e2sar_hip_segreas_batch &x = batches[b];
+        if (x.nEvents == 0 || x.nPackets == 0) continue;
+        if (!x.d_events || !x.d_packets || !x.d_lens) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+        if (((uintptr_t)x.d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+        if ((uint64_t)x.nPackets * (stride >> 4) > 0xFFFFFFFFull) return fail(E2SAR_HIP_ERR_OUT_OF_RANGE, "batch too large");
+        for (uint32_t c = 0; c < b; c++)
+            if (batches[c].d_packets == x.d_packets && batches[c].nPackets)
+                return fail(E2SAR_HIP_ERR_PARAMETER, "batches of one launch need distinct packet buffers");
+        ChainBatch &B = cb.b[cb.nb++];
+        B.events = x.d_events;
+        B.pkts = x.d_packets;
+        B.lens = x.d_lens;
+        B.nEvents = x.nEvents;
+        B.maxPacketsPerEvent = x.maxPacketsPerEvent;
+        B.n = x.nPackets;
+        B.tiles = reinterpret_cast<uint32_t *>(words);        // offset for now
+        words += x.nPackets;
+    }
+    if (cb.nb == 0) return E2SAR_HIP_OK;
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    if (r->tilesBytes < 4ull * words) {
+        HIP_TRY(grow(r->tiles, r->tilesBytes, 4ull * words));
+        HIP_TRY(hipMemset(r->tiles, 0, r->tilesBytes));      // counters start at 0; each launch leaves them 0
+    }
+    for (uint32_t b = 0; b < cb.nb; b++)
+        cb.b[b].tiles = static_cast<uint32_t *>(r->tiles) + reinterpret_cast<uintptr_t>(cb.b[b].tiles);
+    hipError_t e = launch_segreas(cb, lbHdrVersion, maxPldLen, stride, r->dev, now_ms, s);
+    if (e != hipSuccess) return hip_fail(e, "segreas_kernel launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_segment_reassemble_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, uint32_t nEvents,
+                                       uint32_t maxPacketsPerEvent, uint32_t nPackets, int lbHdrVersion,
+                                       uint32_t maxPldLen, uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
+                                       e2sar_hip_reas *r, uint64_t now_ms, void *stream)
+{
+    const e2sar_hip_segreas_batch b{d_events, d_packets, d_lens, nEvents, maxPacketsPerEvent, nPackets, 0u};
+    return segreas(ctx, &b, 1u, lbHdrVersion, maxPldLen, stride, r, now_ms, stream);
+}
+
+int e2sar_hip_segment_reassemble_batches(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches,
+                                         uint32_t nBatches, int lbHdrVersion, uint32_t maxPldLen, uint32_t stride,
+                                         e2sar_hip_reas *r, uint64_t now_ms, void *stream)
+{
+    return segreas(ctx, batches, nBatches, lbHdrVersion, maxPldLen, stride, r, now_ms, stream);
 }
 
 int e2sar_hip_relay_plan(e2sar_hip_reas *r, uint32_t firstRecord, uint32_t maxEvents, size_t maxPldLen,

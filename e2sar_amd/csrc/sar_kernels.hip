@@ -48,6 +48,14 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_SCATTER_NT_LOAD
+// split / pipelined scatter: non-temporal datagram loads.  These forms serve the receive
+// path, whose datagrams were not just written by this GPU: a batch read back cold takes
+// 78.6 instead of 83.5 us (scatter) and 84.8 instead of 88.0 us (scatter + classify), and
+// the hot pipelined round trip gains too (profiles/round2/ab2).  The fused kernel keeps
+// default-policy loads: in the round trip they hit the Infinity Cache (nt: -10 %).
+#define E2SAR_SCATTER_NT_LOAD 1
+#endif
 #ifndef E2SAR_SCATTER_CHUNKS_PER_BLOCK
 #define E2SAR_SCATTER_CHUNKS_PER_BLOCK 1024u
 #endif
@@ -116,6 +124,39 @@ __device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v)
 #endif
 }
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
+
+// Agent-coherent (sc1) forms for bytes handed from one workgroup to another inside a
+// launch (the chained segment -> reassemble form): the producer stores every handed-off
+// byte write-through (sc1), waits for its stores, then signals with an agent-scope atomic;
+// the consumer reads every handed-off byte with sc1 loads (MI355X_MICROARCH.md,
+// inter-workgroup visibility, first hand-off row).  16-byte forms go through a buffer
+// resource whose base is workgroup-uniform (an SGPR operand), with the per-lane offset in
+// a VGPR.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t brsrc(const void *base)
+{
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(base), (short)0, 0x7FFFFFFF, 0x00020000);
+}
+constexpr int kCpolSc1 = 16;
+__device__ __forceinline__ u32x4 ld16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off)
+{
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, kCpolSc1);
+}
+__device__ __forceinline__ void st16_sc1(__amdgpu_buffer_rsrc_t r, uint32_t off, u32x4 v)
+{
+    __builtin_amdgcn_raw_buffer_store_b128(v, r, (int)off, 0, kCpolSc1);
+}
+__device__ __forceinline__ uint32_t ld4_sc1(const uint32_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void st4_sc1(uint32_t *p, uint32_t v)
+{
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint8_t ld1_sc1(const uint8_t *p)
+{
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
 
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every global
 // load and atomic the wave has outstanding; here a classifier's fire-and-forget counter
@@ -234,16 +275,20 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 // event table is built by relay_plan_kernel); blocks of events past it exit.
 // The dword fast path (16-byte loads at dword alignment) is chosen per event from the
 // event's own address and maxPld: a block handles one event, so the choice is uniform.
-template <int U>
-__global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
-                                                     uint32_t blocksPerEvent, int lbVersion,
-                                                     uint32_t maxPld, uint8_t *__restrict__ pkts,
-                                                     uint32_t stride, uint32_t *__restrict__ lens,
-                                                     const uint32_t *__restrict__ dCount)
+//
+// HO (the chained form, segreas_kernel): every datagram byte and length is stored sc1 and,
+// once the block's stores are done, the block adds the number of index-space chunks it
+// covered in each reassembly group's range of datagrams to that group's counter
+// (tiles[slot / tileG]); a group starts when its counter reaches its slots x stride/16.
+template <int U, bool HO>
+__device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict__ events, uint32_t blocksPerEvent,
+                                          int lbVersion, uint32_t maxPld, uint8_t *__restrict__ pkts, uint32_t stride,
+                                          uint32_t *__restrict__ lens, const uint32_t *__restrict__ dCount,
+                                          uint32_t blk, uint32_t tileG, uint32_t *__restrict__ tiles)
 {
     TRACE_AT(1, 0, trace_now());
-    const uint32_t e = blockIdx.x / blocksPerEvent;
-    const uint32_t bx = blockIdx.x - e * blocksPerEvent;
+    const uint32_t e = blk / blocksPerEvent;
+    const uint32_t bx = blk - e * blocksPerEvent;
     if (dCount && e >= *dCount) return;
     const e2sar_hip_seg_event ev = events[e];
     const bool A4 = (((uintptr_t)ev.data | maxPld) & 3u) == 0u;
@@ -258,6 +303,8 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
     lbre_words(hw, lbVersion, ev.entropy, ev.lbTick, ev.dataId, 0u, bytes, ev.eventNum);
     const SegHdr h{hw.w[0], hw.w[1], hw.w[2], hw.w[3], hw.w[4], hw.w[6], hw.w[7], hw.w[8]};
     uint8_t *const out = pkts + (uint64_t)ev.pktBase * stride;
+    const __amdgpu_buffer_rsrc_t outR = brsrc(out + 16ull * j0);        // HO stores only
+    (void)outR;
     const uint8_t *const safe = reinterpret_cast<const uint8_t *>(events + e);   // >= 16 valid bytes
     const float rspc = 1.0f / (float)spc;
 
@@ -287,7 +334,10 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
             const uint32_t c = j - k * spc;
             const uint32_t off = k * maxPld;
             const uint32_t L = (bytes - off > maxPld) ? maxPld : bytes - off;
-            if (c == 0u && lens) lens[ev.pktBase + k] = kLBREHdrLen + L;
+            if (c == 0u && lens) {
+                if (HO) st4_sc1(lens + ev.pktBase + k, kLBREHdrLen + L);
+                else lens[ev.pktBase + k] = kLBREHdrLen + L;
+            }
             if (16u * c < kLBREHdrLen + L) {          // else: chunk wholly past the datagram end
                 jj[u] = j;
                 cc[u] = c;
@@ -339,7 +389,26 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
         } else {
             o = u32x4{h.w0, h.w1, h.w2, h.w3};
         }
-        st16(out + 16u * jj[u], o);
+        if (HO) st16_sc1(outR, 16u * (jj[u] - j0), o);
+        else st16(out + 16u * jj[u], o);
+    }
+    if (HO) {
+        // every storing wave waits for its write-through stores, then one wave signals for
+        // the workgroup behind the barrier
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const uint32_t j1 = (j0 + (uint32_t)(kBlock * U) < nch) ? j0 + (uint32_t)(kBlock * U) : nch;
+            const uint64_t s0 = (uint64_t)ev.pktBase + j0 / spc, s1 = (uint64_t)ev.pktBase + (j1 - 1u) / spc;
+            const uint64_t t0 = s0 / tileG, t1 = s1 / tileG;
+            for (uint64_t t = t0 + (threadIdx.x & 63u); t <= t1; t += 64u) {
+                const uint64_t tlo = t * tileG, thi = tlo + tileG;        // slots of group t
+                const uint64_t clo = (tlo > ev.pktBase) ? (tlo - ev.pktBase) * spc : 0u;
+                const uint64_t chi = (thi - ev.pktBase) * spc;            // thi > s0 >= pktBase
+                const uint64_t lo = clo > j0 ? clo : j0, hi = chi < j1 ? chi : j1;
+                __hip_atomic_fetch_add(tiles + t, (uint32_t)(hi - lo), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
+        }
     }
 #if E2SAR_TRACE
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -347,6 +416,17 @@ __global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *
     TRACE_AT(1, 2, trace_hwid());
     TRACE_AT(1, 3, trace_now());
 #endif
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
+                                                     uint32_t blocksPerEvent, int lbVersion,
+                                                     uint32_t maxPld, uint8_t *__restrict__ pkts,
+                                                     uint32_t stride, uint32_t *__restrict__ lens,
+                                                     const uint32_t *__restrict__ dCount)
+{
+    seg_block<U, false>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount, blockIdx.x, 1u,
+                        nullptr);
 }
 
 // ---------------------------------------------------------------------------------
@@ -557,11 +637,21 @@ struct RawHdr {
     uint32_t re4;    // RE header dword 4 (eventNum low word)
 };
 
+template <bool HO = false>
 __device__ __forceinline__ RawHdr load_hdr(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t p)
 {
     const uint8_t *re = pkts + (uint64_t)p * stride + (R.withLB ? kLBHdrLen : 0u);   // 16-byte aligned
     RawHdr h;
+    if (HO) {       // bytes handed off inside the launch (chained form): sc1 loads
+        h.len = ld4_sc1(lens + p);
+        h.re.x = ld4_sc1(reinterpret_cast<const uint32_t *>(re));
+        h.re.y = ld4_sc1(reinterpret_cast<const uint32_t *>(re + 4));
+        h.re.z = ld4_sc1(reinterpret_cast<const uint32_t *>(re + 8));
+        h.re.w = ld4_sc1(reinterpret_cast<const uint32_t *>(re + 12));
+        h.re4 = ld4_sc1(reinterpret_cast<const uint32_t *>(re + 16));
+        return h;
+    }
     h.len = lens[p];
     h.re = ld16(re);
     h.re4 = ld4(re + 16);
@@ -833,6 +923,7 @@ __device__ __forceinline__ uint32_t da_window(uint32_t c, uint32_t a, uint32_t h
 // Store destination-aligned chunk c (loaded from the window of da_window) of the datagram
 // at dgram: whole aligned 16-byte stores inside the payload, dwords at its two edges,
 // bytes for a sub-dword event tail, byte copies for a payload that is not dword-congruent.
+template <bool HO = false>
 __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, const uint8_t *dgram, uint32_t stride)
 {
     const uint32_t a = (uint32_t)pi.dst & 15u;
@@ -855,7 +946,7 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
         }
     } else {
         const uint8_t *s = dgram + pi.hl + 16u * c - a;                // + lo >= hl
-        for (uint32_t b = lo; b < hi; b++) st1(D + b, ld1(s + b));
+        for (uint32_t b = lo; b < hi; b++) st1(D + b, HO ? ld1_sc1(s + b) : ld1(s + b));
     }
 }
 
@@ -877,7 +968,9 @@ struct ReasGroupLds {
 //   4. every thread stores its chunks (da_store), then loads and stores the rest round by
 //      round (U chunks of 16 bytes per thread per round);
 //   5. the run tails complete events (their atomic results are consumed last).
-template <int U>
+// HO: the chained form -- every datagram byte and length is read with sc1 loads (they were
+// stored write-through by seg_block in the same launch).
+template <int U, bool HO = false>
 __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
                                            uint32_t g, ReasGroupLds &L)
@@ -890,7 +983,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 
     TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
-    const RawHdr raw = load_hdr(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
+    const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
     TRACE_WAIT();
     TRACE_AT(2, 0, trace_now());
 
@@ -898,6 +991,8 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     const uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
+    const __amdgpu_buffer_rsrc_t bpkR = brsrc(bpk);                     // HO loads only
+    (void)bpkR;
     // chunk i -> (datagram, chunk within it); recomputed at store time rather than kept
     // live across the classification (register pressure sets this kernel's occupancy)
     auto split_chunk = [&](uint32_t i, uint32_t &p, uint32_t &c) {
@@ -919,7 +1014,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
             const uint32_t a = __shfl(gPhase, (int)p), plen = __shfl(gPlen, (int)p);
             uint32_t off = 0, sh;
             if (i < nch && 16u * c < a + plen && (a & 3u) == 0u) off = p * stride + da_window(c, a, hl, stride, sh);
-            xs[u] = ld16(bpk + off);
+            xs[u] = HO ? ld16_sc1(bpkR, off) : ld16(bpk + off);
         }
     };
     auto store = [&](uint32_t r0, const u32x4(&xs)[U]) {
@@ -929,7 +1024,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
             if (i >= nch) continue;
             uint32_t p, c;
             split_chunk(i, p, c);
-            da_store(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
+            da_store<HO>(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
         }
     };
     u32x4 x[U];
@@ -1015,6 +1110,64 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(Reas
 }
 
 // ---------------------------------------------------------------------------------
+// chained form: segmentation of a batch and reassembly of the same datagrams in ONE launch.
+// Workgroups [0, nSeg) are seg_kernel blocks (HO: write-through stores, then a per-group
+// counter add); workgroups [nSeg, nSeg + groups) are reas_kernel groups, each of which
+// waits until its counter shows every datagram of its range written, then runs as in
+// reas_kernel with sc1 loads.  A group waits only on blocks with lower indices, which
+// are dispatched before it and never wait, so the grid always drains; the wait is also
+// bounded (2 s, error flag bit 4), so a miscount can never hang the device.  The group
+// resets its counter for the next launch.  What this buys over two launches: the
+// reassembly groups start while the last segmentation blocks finish (no kernel boundary,
+// no half-empty tail between the two kernels).
+
+__device__ __forceinline__ void wait_group_ready(const ReasDev &R, uint32_t *tiles, uint32_t g, uint32_t expect)
+{
+    if (threadIdx.x == 0) {
+        uint32_t *t = tiles + g;
+        uint64_t t0 = 0;
+        for (uint32_t it = 0;; it++) {
+            const uint32_t v = ld4_sc1(t);
+            if (v >= expect) {
+                if (v != expect) atomicOr(&R.ctl->errorFlags, 32u);           // over-count
+                break;
+            }
+            const uint64_t now = __builtin_amdgcn_s_memrealtime();           // 100 MHz
+            if (it == 0) t0 = now;
+            else if (now - t0 > 200000000ull) {
+                atomicOr(&R.ctl->errorFlags, 16u);                           // wait timed out
+                break;
+            }
+            __builtin_amdgcn_s_sleep(2);
+        }
+        st4_sc1(t, 0u);
+    }
+    __syncthreads();
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(ChainBatches cb, int lbVersion,
+                                                                              uint32_t maxPld, uint32_t stride,
+                                                                              ReasDev R, uint64_t now)
+{
+    __shared__ ReasGroupLds L;
+    // grid: [seg(0) | reas(0) | seg(1) | reas(1) | ...]; a reassembly group depends only on
+    // segmentation blocks of its own batch, all of which have lower indices
+    uint32_t b = 0;
+    while (b + 1u < cb.nb && blockIdx.x >= cb.b[b + 1u].start) b++;
+    const ChainBatch &B = cb.b[b];
+    const uint32_t local = blockIdx.x - B.start;
+    if (local < B.nSeg) {
+        seg_block<U, true>(B.events, B.bpe, lbVersion, maxPld, B.pkts, stride, B.lens, nullptr, local, B.G, B.tiles);
+        return;
+    }
+    const uint32_t g = local - B.nSeg;
+    const uint32_t slots = (B.n - g * B.G < B.G) ? B.n - g * B.G : B.G;
+    wait_group_ready(R, B.tiles, g, slots * (stride >> 4));
+    reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L);
+}
+
+// ---------------------------------------------------------------------------------
 // reassembly as two phases: classify (headers only, latency-bound) then scatter (bytes
 // only, bandwidth-bound).  Each phase is a launch of its own, or -- the pipelined form --
 // one launch scatters batch b while other workgroups of the same grid classify batch
@@ -1088,7 +1241,11 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
             else if ((p + 1u) * spc <= ic) p++;
             pp[u] = p;
             cc[u] = ic - p * spc;
+#if E2SAR_SCATTER_NT_LOAD
+            x[u] = ld16_nt(bpk + (uint64_t)p * stride + 16u * cc[u]);
+#else
             x[u] = ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
+#endif
         }
     };
     issue(0);
@@ -1561,6 +1718,14 @@ static uint32_t occupancy_lds(const char *var)
     return (x > 0 && x <= 65536) ? (uint32_t)x : 0u;
 }
 
+static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
+{
+    const char *v = getenv(var);
+    if (!v) return dflt;
+    const long x = atol(v);
+    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
+}
+
 static uint32_t scatter_group_size(uint32_t stride)
 {
     // datagrams per scatter workgroup: at most E2SAR_SCATTER_CHUNKS_PER_BLOCK 16-byte chunks
@@ -1571,16 +1736,9 @@ static uint32_t scatter_group_size(uint32_t stride)
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
     while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK) G >>= 1;
-    return G;
+    return env_u32("E2SAR_SCATTER_G", G, 1, 64);       // A/B knob: exact datagrams per workgroup
 }
 
-static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
-{
-    const char *v = getenv(var);
-    if (!v) return dflt;
-    const long x = atol(v);
-    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
-}
 
 // Workgroups of reas_kernel<U> the current device holds at once (0 if unknown), per device.
 template <int U>
@@ -1600,11 +1758,9 @@ static uint32_t reas_resident_groups()
     return c;
 }
 
-hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
+static uint32_t reas_group_size(uint32_t n, uint32_t stride)
 {
     constexpr int U = E2SAR_REAS_U;
-    if (n == 0) return hipSuccess;
     // datagrams per workgroup: at most E2SAR_REAS_CHUNKS 16-byte chunks (A/B knob), <= 64.
     // (A/B: at MTU 1500 2K-chunk groups lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
     // 8 MiB events 4K chunks (4 datagrams per group) lose 27 % to 9K-18K: per-event counter
@@ -1634,8 +1790,39 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
             G = best;
         }
     }
-    G = env_u32("E2SAR_REAS_G", G, 1, 64);             // A/B knob: exact datagrams per workgroup
+    return env_u32("E2SAR_REAS_G", G, 1, 64);          // A/B knob: exact datagrams per workgroup
+}
+
+hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (n == 0) return hipSuccess;
+    const uint32_t G = reas_group_size(n, stride);
     hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G);
+    return hipGetLastError();
+}
+
+hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint32_t stride, const ReasDev &R,
+                          uint64_t now, hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (cb.nb == 0 || cb.nb > kChainMaxBatches) return hipErrorInvalidValue;
+    uint64_t grid = 0;
+    for (uint32_t b = 0; b < cb.nb; b++) {
+        ChainBatch &B = cb.b[b];
+        const uint64_t chunks = (uint64_t)B.maxPacketsPerEvent * (stride >> 4);
+        if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
+        B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * U) : 0u;
+        B.G = B.n ? reas_group_size(B.n, stride) : 1u;
+        B.start = (uint32_t)grid;
+        B.nSeg = B.bpe * B.nEvents;
+        grid += (uint64_t)B.nSeg + (B.n ? cdiv(B.n, B.G) : 0u);
+        if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    }
+    if (grid == 0) return hipSuccess;
+    hipLaunchKernelGGL((segreas_kernel<U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, cb, lbVersion, maxPld, stride,
+                       R, now);
     return hipGetLastError();
 }
 

@@ -163,6 +163,25 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
                              uint32_t *d_counts, hipStream_t stream);
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
+// Chained form: segment each batch and reassemble the same datagrams, up to
+// kChainMaxBatches batches in one launch (segreas_kernel).  Batch b: nEvents descriptors at
+// events (pktBase from seg_plan), n datagrams into pkts/lens, tiles = n zeroed words (left
+// zeroed by the launch); batches use distinct packet buffers.
+constexpr uint32_t kChainMaxBatches = 8;
+struct ChainBatch {
+    const e2sar_hip_seg_event *events;
+    uint8_t *pkts;
+    uint32_t *lens;
+    uint32_t *tiles;
+    uint32_t nEvents, maxPacketsPerEvent, n;
+    uint32_t start, nSeg, bpe, G;           // filled by launch_segreas
+};
+struct ChainBatches {
+    ChainBatch b[kChainMaxBatches];
+    uint32_t nb;
+};
+hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint32_t stride, const ReasDev &R,
+                          uint64_t now, hipStream_t stream);
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                                 uint32_t n, uint64_t now, void *work, hipStream_t stream);
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,

@@ -144,6 +144,35 @@ class DeviceSegmenter:
             C.c_void_p(_stream_handle(stream))))
         return plan.total_packets
 
+    def segment_reassemble(self, plan: SegPlan, packets: torch.Tensor, lens: torch.Tensor,
+                           reas: "DeviceReassembler", now_ms: int = 0,
+                           stream: Optional[torch.cuda.Stream] = None) -> int:
+        """Chained form: segment the batch and reassemble the same datagrams into `reas`
+        in one launch (e2sar_hip_segment_reassemble_batch)."""
+        if packets.numel() < plan.total_packets * self.stride or lens.numel() < plan.total_packets:
+            raise ValueError("packet buffer too small")
+        check(lib().e2sar_hip_segment_reassemble_batch(
+            self.ctx.handle, C.c_void_p(plan.device.data_ptr()), plan.n_events, plan.max_packets_per_event,
+            plan.total_packets, self.lb_hdr_version, self.max_pld, C.c_void_p(packets.data_ptr()), self.stride,
+            C.c_void_p(lens.data_ptr()), reas._h, int(now_ms), C.c_void_p(_stream_handle(stream))))
+        return plan.total_packets
+
+    def segment_reassemble_batches(self, plans: Sequence[SegPlan], bufs: Sequence[tuple],
+                                   reas: "DeviceReassembler", now_ms: int = 0,
+                                   stream: Optional[torch.cuda.Stream] = None) -> int:
+        """Chained form over several batches in one launch (at most 8;
+        e2sar_hip_segment_reassemble_batches); bufs[k] = (packets, lens) of plans[k], all distinct."""
+        arr = (_capi.SegReasBatch * max(1, len(plans)))()
+        for k, (p, (pk, ln)) in enumerate(zip(plans, bufs)):
+            if pk.numel() < p.total_packets * self.stride or ln.numel() < p.total_packets:
+                raise ValueError("packet buffer too small")
+            arr[k] = _capi.SegReasBatch(p.device.data_ptr(), pk.data_ptr(), ln.data_ptr(), p.n_events,
+                                        p.max_packets_per_event, p.total_packets, 0)
+        check(lib().e2sar_hip_segment_reassemble_batches(
+            self.ctx.handle, arr, len(plans), self.lb_hdr_version, self.max_pld, self.stride, reas._h, int(now_ms),
+            C.c_void_p(_stream_handle(stream))))
+        return sum(p.total_packets for p in plans)
+
     def segment_device(self, events: torch.Tensor, counts: torch.Tensor, max_events: int,
                        max_packets_per_event: int, packets: torch.Tensor, lens: Optional[torch.Tensor],
                        stream: Optional[torch.cuda.Stream] = None) -> None:

@@ -217,7 +217,9 @@ typedef struct e2sar_hip_reas_stats {
     uint64_t arenaUsed;
     uint64_t tableUsed;          /* slots ever claimed since the last recycle */
     uint32_t errorFlags;         /* bit0 table full, bit1 arena full, bit2 probe timeout,
-                                    bit3 scatter record outside the arena (bad work buffer) */
+                                    bit3 scatter record outside the arena (bad work buffer),
+                                    bit4 chained form: a group's datagrams never all written
+                                    (wait timed out), bit5 chained form: counter over-count */
     uint32_t reserved;
 } e2sar_hip_reas_stats;
 
@@ -289,6 +291,40 @@ int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream);
 /* Zero the statistics counters (event counters, per-datagram counters, error flags).
  * Completed and lost records not yet polled stay queued.  Asynchronous. */
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
+
+/* Chained round trip (BASELINE config 2's device-resident step) in ONE launch: segment
+ * the batch (as e2sar_hip_segment_batch, d_lens required) and reassemble the same
+ * nPackets datagrams into r (as e2sar_hip_reassemble_batch).  Reassembly workgroups start
+ * as soon as the segmentation workgroups that write their datagrams have published them
+ * (write-through stores + per-group agent-scope counters held by r), so the two stages
+ * overlap at their seam instead of meeting at a kernel boundary.  Results are those of
+ * the two calls in sequence.  nPackets = seg_plan's total; r created withLBHeader, not
+ * REFERENCE_ORDER.  The first call for a larger nPackets allocates r's counters
+ * (synchronous; outside graph capture).  A group whose datagrams never all arrive (a bad
+ * descriptor table) stops waiting after 2 s and sets errorFlags bit 4.  Asynchronous.
+ * Replaces _send (e2sarDPSegmenter.cpp:660-871) followed by the receive body
+ * (e2sarDPReassembler.cpp:335-427) on the same events. */
+int e2sar_hip_segment_reassemble_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, uint32_t nEvents,
+                                       uint32_t maxPacketsPerEvent, uint32_t nPackets, int lbHdrVersion,
+                                       uint32_t maxPldLen, uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
+                                       e2sar_hip_reas *r, uint64_t now_ms, void *stream);
+
+/* Several batches (at most 8) chained in one launch: batch b's reassembly groups wait on
+ * batch b's segmentation only, and batch b+1's segmentation starts while batch b's
+ * reassembly finishes.  Each batch needs its own packet and length buffers.  Results are
+ * those of the batches' segment_batch + reassemble_batch calls in order. */
+typedef struct e2sar_hip_segreas_batch {
+    const e2sar_hip_seg_event *d_events;   /* descriptors on the device, pktBase from seg_plan */
+    uint8_t *d_packets;
+    uint32_t *d_lens;
+    uint32_t nEvents;
+    uint32_t maxPacketsPerEvent;
+    uint32_t nPackets;
+    uint32_t reserved;
+} e2sar_hip_segreas_batch;
+int e2sar_hip_segment_reassemble_batches(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches,
+                                         uint32_t nBatches, int lbHdrVersion, uint32_t maxPldLen, uint32_t stride,
+                                         e2sar_hip_reas *r, uint64_t now_ms, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* relay (BASELINE config 5: receive -> reassemble -> segment -> send on one GPU): the    */

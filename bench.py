@@ -202,7 +202,27 @@ def cpu_baseline(args, budget_s: float):
             "sample": f"{pT} passes on {T} threads in {dT:.1f} s; {what}",
             "host": {**info, "threads_used": T,
                      "cap": "min(16, OMP_NUM_THREADS, sched_getaffinity): the GPU box's CPU share per GPU"},
-            "single_core": {"value": round(v1, 4), "cores": 1, "sample": f"{p1} passes in {d1:.1f} s"}}
+            "single_core": {"value": round(v1, 4), "cores": 1, "sample": f"{p1} passes in {d1:.1f} s"},
+            "config1_loopback": cpu_loopback(args, min(5.0, budget_s))}
+
+
+def cpu_loopback(args, seconds: float):
+    """BASELINE config 1 (bin/e2sar_perf loopback on the host CPU, one Segmenter and one
+    Reassembler thread): oracle/build/e2o_loopback -- the oracle's SAR path with one sendto
+    per datagram and one recvfrom per datagram over UDP 127.0.0.1, the sender keeping at most
+    half a receive buffer of datagrams in flight (the fastest lossless rate)."""
+    exe = os.path.join(ROOT, "oracle", "build", "e2o_loopback")
+    if not os.path.exists(exe):
+        return None
+    try:
+        out = subprocess.run([exe, str(args.event_bytes), str(args.mtu), str(seconds)], capture_output=True,
+                             text=True, timeout=seconds + 30)
+        res = json.loads(out.stdout.strip().splitlines()[-1])
+    except (OSError, ValueError, IndexError, subprocess.TimeoutExpired):
+        return None
+    res["what"] = ("1 segmenter thread + 1 reassembler thread, UDP loopback, sendto/recvfrom per datagram, "
+                   "oracle segment/receive body; threads 2 (kind port)")
+    return res
 
 
 def graph_steps(args) -> int:

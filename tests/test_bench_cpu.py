@@ -1,9 +1,12 @@
 """bench.py's CPU-side pieces on the CPU: argument defaults (the driver's contract) and the
 cpu_baseline leg (the oracle on host threads, a tiny budget here)."""
 import argparse
+import os
 import sys
 
 import bench
+
+ROOT = bench.ROOT
 
 
 def test_defaults_are_the_headline_workload(monkeypatch):
@@ -51,3 +54,16 @@ def test_graph_steps_divides_the_timed_steps():
 def test_cpu_info_fields():
     info = bench.host_cpu_info()
     assert info["nproc"] >= 1 and 1 <= info["allowed"] <= info["nproc"]
+
+
+def test_config1_cpu_loopback_runs():
+    # BASELINE config 1 (the oracle's SAR path over UDP loopback, one sender + one receiver
+    # thread) as bench.py's cpu_baseline leg runs it: events flow and arrive intact
+    import json
+    import subprocess
+    exe = os.path.join(ROOT, "oracle", "build", "e2o_loopback")
+    if not os.path.exists(exe):
+        subprocess.run(["make", "-C", os.path.join(ROOT, "oracle")], check=True)
+    out = subprocess.run([exe, "65536", "1500", "1"], capture_output=True, text=True, timeout=60, check=True)
+    res = json.loads(out.stdout.strip().splitlines()[-1])
+    assert res["events"] > 0 and res["bad_events"] == 0 and res["GiBps"] > 0

@@ -349,9 +349,11 @@ int main(int argc, char **argv)
         Segmenter s(uri, o.dataId, o.src, sflags);
         printf("Event size is %zu bytes, sending %zu events, MTU %u\n", o.length, o.num, s.getMTU());
         sendEvents(s, o);
-        // wait for the receiver (bounded: the reassembly timeout plus a margin)
+        // wait for the receiver threads to take every event off the queue (they set `stop`
+        // at o.num), bounded by the reassembly timeout plus a margin.  (Waiting on the device
+        // counters instead raced the delivery of the last completed events.)
         const auto deadline = clk::now() + std::chrono::milliseconds(2000 + 2 * o.timeoutMs);
-        while (clk::now() < deadline && r.getStats().eventSuccess + r.getStats().reassemblyLoss < o.num)
+        while (clk::now() < deadline && !stop.load())
             std::this_thread::sleep_for(std::chrono::milliseconds(1));
         stop.store(true);
         rt.join();

@@ -102,6 +102,7 @@ struct Reassembler::Impl {
     std::vector<std::thread> recvThreads;
     std::thread devThread;
     std::atomic<bool> stop{false};
+    std::atomic<bool> devWaiting{false};   // the device thread is waiting for a batch
     std::atomic<int> recvActive{0};
     bool started = false;
     e2sar_hip_reas_stats lastStats{};
@@ -263,6 +264,23 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
     const size_t S = flags.recvStride;
     std::vector<mmsghdr> mv(cap);
     std::vector<iovec> iv(cap);
+    // the message vector of a batch points at its slots; built once per batch (recvmmsg only
+    // writes msg_len / msg_flags back), so a call that returns few datagrams costs no setup
+    const Batch *vecFor = nullptr;
+    auto vectorFor = [&](const Batch *x) {
+        if (vecFor == x) return;
+        for (size_t k = 0; k < cap; k++) {
+            iv[k].iov_base = x->pkts + k * S;
+            iv[k].iov_len = S;
+            mv[k].msg_hdr = msghdr{};
+            mv[k].msg_hdr.msg_iov = &iv[k];
+            mv[k].msg_hdr.msg_iovlen = 1;
+        }
+        vecFor = x;
+    };
+    // E2SAR_RECV_PROFILE=1: where the receive thread's time goes (stderr at exit)
+    static const bool prof = getenv("E2SAR_RECV_PROFILE") != nullptr;
+    uint64_t tPoll = 0, tRecv = 0, tFree = 0, nCalls = 0, nDg = 0, nFlush = 0, tLastDg = 0, t0 = detail::now_us();
     Batch *b = takeFree();
     uint64_t firstUs = 0;
     auto flush = [&]() {
@@ -272,7 +290,9 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
             fullB.push_back(b);
         }
         bFullCv.notify_one();
+        const uint64_t a = prof ? detail::now_us() : 0;
         b = takeFree();
+        if (prof) tFree += detail::now_us() - a, nFlush++;
         firstUs = 0;
     };
     while (!stop) {
@@ -281,7 +301,9 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
             if (!b) continue;
         }
         const int timeout = (b->n > 0) ? std::max(1, flags.batchTimeout_us / 1000) : 10;   // 10 ms like sleep_tv
+        const uint64_t pa = prof ? detail::now_us() : 0;
         const int pr = poll(pf.data(), pf.size(), timeout);
+        if (prof) tPoll += detail::now_us() - pa;
         if (pr < 0) {
             if (errno != EINTR) {
                 dataErrCnt++;
@@ -293,14 +315,14 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
             if (!(pf[i].revents & POLLIN)) continue;
             while (b && b->n < cap) {
                 const size_t room = cap - b->n;
-                for (size_t k = 0; k < room; k++) {
-                    iv[k].iov_base = b->pkts + (b->n + k) * S;
-                    iv[k].iov_len = S;
-                    mv[k].msg_hdr = msghdr{};
-                    mv[k].msg_hdr.msg_iov = &iv[k];
-                    mv[k].msg_hdr.msg_iovlen = 1;
+                vectorFor(b);
+                mmsghdr *const m = mv.data() + b->n;
+                const uint64_t ra = prof ? detail::now_us() : 0;
+                const int r = recvmmsg(fds[i], m, (unsigned)room, MSG_DONTWAIT, nullptr);
+                if (prof) {
+                    tRecv += detail::now_us() - ra, nCalls++, nDg += r > 0 ? (uint64_t)r : 0u;
+                    if (r > 0) tLastDg = detail::now_us() - t0;
                 }
-                const int r = recvmmsg(fds[i], mv.data(), (unsigned)room, MSG_DONTWAIT, nullptr);
                 if (r < 0) {
                     if (errno != EAGAIN && errno != EWOULDBLOCK && errno != EINTR) {
                         dataErrCnt++;
@@ -309,8 +331,8 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
                     break;
                 }
                 for (int k = 0; k < r; k++) {
-                    uint32_t len = mv[k].msg_len;
-                    if (mv[k].msg_hdr.msg_flags & MSG_TRUNC) len = (uint32_t)S + 1;   // device: dataErrCnt
+                    uint32_t len = m[k].msg_len;
+                    if (m[k].msg_hdr.msg_flags & MSG_TRUNC) len = (uint32_t)S + 1;   // device: dataErrCnt
                     b->lens[b->n + k] = len;
                 }
                 perPort[ports[i]]->fetch_add((size_t)r);
@@ -320,8 +342,18 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
                 if (r < (int)room) break;
             }
         }
-        if (b && b->n > 0 && detail::now_us() - firstUs >= (uint64_t)flags.batchTimeout_us) flush();
+        // a partial batch goes after batchTimeout_us only if the device thread is waiting for
+        // one; while it is busy the batch keeps filling (a device cycle costs the same for 100
+        // datagrams as for 1000, so flushing small batches into a backlog caps the rate)
+        if (b && b->n > 0 && devWaiting.load(std::memory_order_relaxed) &&
+            detail::now_us() - firstUs >= (uint64_t)flags.batchTimeout_us)
+            flush();
     }
+    if (prof)
+        fprintf(stderr, "recv thread: %.3f s, poll %.3f s, recvmmsg %.3f s (%llu calls, %llu datagrams), "
+                        "waiting for a free batch %.3f s (%llu batches), last datagram at %.3f s\n",
+                (detail::now_us() - t0) * 1e-6, tPoll * 1e-6, tRecv * 1e-6, (unsigned long long)nCalls,
+                (unsigned long long)nDg, tFree * 1e-6, (unsigned long long)nFlush, tLastDg * 1e-6);
     if (b) {
         if (b->n) {
             std::lock_guard<std::mutex> lk(bMu);
@@ -337,7 +369,11 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
 Reassembler::Impl::Batch *Reassembler::Impl::takeFull(bool wait)
 {
     std::unique_lock<std::mutex> lk(bMu);
-    if (wait) bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
+    if (wait && fullB.empty()) {
+        devWaiting.store(true, std::memory_order_relaxed);
+        bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
+        devWaiting.store(false, std::memory_order_relaxed);
+    }
     if (fullB.empty()) return nullptr;
     Batch *b = fullB.front();
     fullB.pop_front();
@@ -464,8 +500,14 @@ void Reassembler::Impl::devBody()
     const uint32_t stride = (uint32_t)flags.recvStride;
     bool kernelInFlight = false;       // a launched batch whose results are not yet drained
     int cur = 0;                       // device set of the next copy
+    static const bool prof = getenv("E2SAR_RECV_PROFILE") != nullptr;
+    uint64_t pT0 = detail::now_us(), pWait = 0, pPoll = 0, pGather = 0, pUpkeep = 0, pLaunch = 0, pCycles = 0,
+             pBatches = 0, pDg = 0, pEvents = 0, pLastEv = 0;
+    auto tick = [&]() { return prof ? detail::now_us() : 0; };
     while (true) {
+        uint64_t ta = tick();
         Batch *b = takeFull(!kernelInFlight);
+        if (prof) pWait += tick() - ta, pCycles++, pBatches += b ? 1 : 0, pDg += b ? b->n : 0;
         if (!b && !kernelInFlight && stop && recvActive.load() == 0) {
             std::lock_guard<std::mutex> lk(bMu);
             if (fullB.empty()) break;
@@ -482,7 +524,9 @@ void Reassembler::Impl::devBody()
             if (rc) lastErr = static_cast<E2SARErrorc>(-rc);
         }
         uint32_t n = 0;
+        ta = tick();
         if (e2sar_hip_reas_poll(reas, recs.data(), (uint32_t)recs.size(), &n) != 0) lastErr = E2SARErrorc::SystemError;
+        if (prof) pPoll += tick() - ta, pEvents += n, pLastEv = n ? tick() - pT0 : pLastEv;
         if (b) giveBack(b);                                   // its bytes are on the device now
         kernelInFlight = false;
         e2sar_hip_reas_stats st{};
@@ -497,6 +541,7 @@ void Reassembler::Impl::devBody()
         const bool gcDue = now - lastGc >= (uint64_t)flags.eventTimeout_ms;
         const bool upkeepDue = haveStats && needsUpkeep(st);
         uint32_t done = 0;
+        ta = tick();
         if (gcDue || upkeepDue) {
             // every completed event leaves the arena before the GC pass, a recycle or a compaction
             for (gatherFinish(0, upto), done = upto; done < n; done = upto) {
@@ -510,6 +555,8 @@ void Reassembler::Impl::devBody()
             }
             if (upkeepDue) upkeep(st);
         }
+        if (prof) pUpkeep += tick() - ta;
+        ta = tick();
         if (b) {
             int rc = e2sar_hip_stream_wait_event(ctx, nullptr, d.h2dDone);
             if (rc == 0) rc = e2sar_hip_reassemble_batch(reas, d.pkts, stride, d.lens, bn, bnow, nullptr);
@@ -517,6 +564,8 @@ void Reassembler::Impl::devBody()
             else kernelInFlight = true;
             cur ^= 1;
         }
+        if (prof) pLaunch += tick() - ta;
+        ta = tick();
         if (done < n) {                                // while that kernel runs
             gatherFinish(done, upto);
             for (done = upto; done < n; done = upto) {
@@ -524,7 +573,14 @@ void Reassembler::Impl::devBody()
                 gatherFinish(done, upto);
             }
         }
+        if (prof) pGather += tick() - ta;
     }
+    if (prof)
+        fprintf(stderr, "device thread: %.3f s, %llu cycles (%llu batches, %llu datagrams, %llu events), waiting %.3f s, "
+                        "poll %.3f s, upkeep/GC %.3f s, copy+launch %.3f s, gather %.3f s, last event at %.3f s\n",
+                (detail::now_us() - pT0) * 1e-6, (unsigned long long)pCycles, (unsigned long long)pBatches,
+                (unsigned long long)pDg, (unsigned long long)pEvents, pWait * 1e-6, pPoll * 1e-6, pUpkeep * 1e-6,
+                pLaunch * 1e-6, pGather * 1e-6, pLastEv * 1e-6);
     uint32_t n = 0;
     if (e2sar_hip_reas_poll(reas, recs.data(), (uint32_t)recs.size(), &n) == 0 && n) {
         uint8_t *arena = e2sar_hip_reas_arena(reas);

@@ -102,7 +102,6 @@ struct Reassembler::Impl {
     std::vector<std::thread> recvThreads;
     std::thread devThread;
     std::atomic<bool> stop{false};
-    std::atomic<bool> devWaiting{false};   // the device thread is waiting for a batch
     std::atomic<int> recvActive{0};
     bool started = false;
     e2sar_hip_reas_stats lastStats{};
@@ -188,7 +187,11 @@ void Reassembler::Impl::setup(size_t nThreads)
     if (rc == 0) rc = e2sar_hip_event_create(ctx, &gatherDone);
     stageBytes = std::max<size_t>(size_t(64) << 20, 2 * flags.recvBatch * flags.recvStride);
     if (rc == 0) rc = e2sar_hip_host_alloc(stageBytes, reinterpret_cast<void **>(&stage));
-    const size_t nb = 2 * numRecvThreads + 2;
+    // host batches: two per receive thread being filled / queued, two on their way to the
+    // device, and slack so a receive thread never waits for one while the device thread
+    // still holds batches whose copies are done but not yet handed back (MTU 9000 loopback
+    // lost datagrams with 4: 0.1 s of waiting for a free batch)
+    const size_t nb = 2 * numRecvThreads + 6;
     batches.resize(nb);
     for (auto &b : batches) {
         if (rc == 0) rc = e2sar_hip_host_alloc(flags.recvBatch * flags.recvStride, reinterpret_cast<void **>(&b.pkts));
@@ -281,6 +284,11 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
     // E2SAR_RECV_PROFILE=1: where the receive thread's time goes (stderr at exit)
     static const bool prof = getenv("E2SAR_RECV_PROFILE") != nullptr;
     uint64_t tPoll = 0, tRecv = 0, tFree = 0, nCalls = 0, nDg = 0, nFlush = 0, tLastDg = 0, t0 = detail::now_us();
+    static const uint64_t spinUs = [] {
+        const char *v = getenv("E2SAR_RECV_SPIN_US");
+        return v ? (uint64_t)strtoull(v, nullptr, 10) : 200ull;
+    }();
+    uint64_t lastData = 0;
     Batch *b = takeFree();
     uint64_t firstUs = 0;
     auto flush = [&]() {
@@ -301,9 +309,18 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
             if (!b) continue;
         }
         const int timeout = (b->n > 0) ? std::max(1, flags.batchTimeout_us / 1000) : 10;   // 10 ms like sleep_tv
-        const uint64_t pa = prof ? detail::now_us() : 0;
-        const int pr = poll(pf.data(), pf.size(), timeout);
-        if (prof) tPoll += detail::now_us() - pa;
+        // while datagrams keep coming, stay awake and poll the sockets with non-blocking
+        // recvmmsg for up to spinUs after the last one: a sleeping receiver costs the
+        // sending side one wakeup per datagram (loopback: half the datagram rate)
+        int pr;
+        if (lastData && detail::now_us() - lastData < spinUs) {
+            for (auto &p : pf) p.revents = POLLIN;
+            pr = (int)pf.size();
+        } else {
+            const uint64_t pa = prof ? detail::now_us() : 0;
+            pr = poll(pf.data(), pf.size(), timeout);
+            if (prof) tPoll += detail::now_us() - pa;
+        }
         if (pr < 0) {
             if (errno != EINTR) {
                 dataErrCnt++;
@@ -336,18 +353,17 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
                     b->lens[b->n + k] = len;
                 }
                 perPort[ports[i]]->fetch_add((size_t)r);
+                if (r > 0) lastData = detail::now_us();
                 if (b->n == 0 && r > 0) firstUs = detail::now_us();
                 b->n += (uint32_t)r;
                 if (b->n == cap) flush();
                 if (r < (int)room) break;
             }
         }
-        // a partial batch goes after batchTimeout_us only if the device thread is waiting for
-        // one; while it is busy the batch keeps filling (a device cycle costs the same for 100
-        // datagrams as for 1000, so flushing small batches into a backlog caps the rate)
-        if (b && b->n > 0 && devWaiting.load(std::memory_order_relaxed) &&
-            detail::now_us() - firstUs >= (uint64_t)flags.batchTimeout_us)
-            flush();
+        // (A/B, dropped: flushing a partial batch only while the device thread waits for one
+        // lost jumbo datagrams at MTU 9000 -- the batch then grows to 9 MB behind a busy
+        // device -- and gained nothing at 1500)
+        if (b && b->n > 0 && detail::now_us() - firstUs >= (uint64_t)flags.batchTimeout_us) flush();
     }
     if (prof)
         fprintf(stderr, "recv thread: %.3f s, poll %.3f s, recvmmsg %.3f s (%llu calls, %llu datagrams), "
@@ -369,11 +385,7 @@ void Reassembler::Impl::recvBody(size_t, std::vector<int> fds, std::vector<uint1
 Reassembler::Impl::Batch *Reassembler::Impl::takeFull(bool wait)
 {
     std::unique_lock<std::mutex> lk(bMu);
-    if (wait && fullB.empty()) {
-        devWaiting.store(true, std::memory_order_relaxed);
-        bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
-        devWaiting.store(false, std::memory_order_relaxed);
-    }
+    if (wait) bFullCv.wait_for(lk, std::chrono::milliseconds(10), [&] { return stop.load() || !fullB.empty(); });
     if (fullB.empty()) return nullptr;
     Batch *b = fullB.front();
     fullB.pop_front();

@@ -323,9 +323,18 @@ result<int> Segmenter::Impl::sendBatch(std::vector<Item> &items)
             }
             paceNext += std::chrono::nanoseconds((int64_t)((double)items[i].bytes * 8.0 / flags.rateGbps));
         }
+        // at most sendChunk datagrams per call: the kernel hands a loopback or local
+        // receiver's datagrams over when the call returns, and a whole event's worth in one
+        // call (731 at MTU 1500) overruns its per-CPU backlog; short calls keep the sender
+        // at the rate the receiving side drains
+        static const uint32_t sendChunk = [] {
+            const char *v = getenv("E2SAR_SEND_CHUNK");
+            const unsigned long x = v ? strtoul(v, nullptr, 10) : 64ul;
+            return (uint32_t)(x ? x : 0xFFFFFFFFul);
+        }();
         uint32_t sent = 0;
         while (sent < n) {
-            const int r = sendmmsg(fds[s], mv.data() + sent, n - sent, 0);
+            const int r = sendmmsg(fds[s], mv.data() + sent, std::min(n - sent, sendChunk), 0);
             if (r < 0) {
                 if (errno == EINTR) continue;
                 if (errno == EAGAIN || errno == ENOBUFS) {

@@ -344,10 +344,10 @@ int main(int argc, char **argv)
         // loopback: receiver thread + sender here; end-to-end goodput from the first
         // addToSendQueue to the last validated event
         RecvResult rr;
-        const auto t0 = clk::now();
         std::thread rt([&] { rr = recvEventsMT(r, o, o.num, stop); });
         Segmenter s(uri, o.dataId, o.src, sflags);
         printf("Event size is %zu bytes, sending %zu events, MTU %u\n", o.length, o.num, s.getMTU());
+        const auto t0 = clk::now();           // after both sides are set up (GPU contexts, buffers)
         sendEvents(s, o);
         // wait for the receiver threads to take every event off the queue (they set `stop`
         // at o.num), bounded by the reassembly timeout plus a margin.  (Waiting on the device

@@ -36,6 +36,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
+XGMI_PEAK_GBS = 7 * 153.0  # per GPU, 7 xGMI links x ~153 GB/s (point to point)
 METRIC = "GiB/s event payload segmented+reassembled, device-resident, 1/2/4/8 MI355X"
 
 
@@ -363,6 +364,8 @@ def main():
             timed("reas_classify_kernel", R.classify, pk, stride, ln, n, w, stream=stream)
             timed("reas_scatter_kernel", R.scatter, pk, stride, n, w, stream=stream)
 
+    last_counts = []
+
     def step_spread():
         """Datagrams land on this rank whatever their owner: route by owner on the GPU, one
         all-to-all-v over RCCL, reassemble what this rank owns."""
@@ -372,6 +375,7 @@ def main():
         spk, sln, cnt = timed("route_kernels", router.route, lpk, lln, step_pk)
         if world > 1:
             counts = [int(c) for c in cnt.tolist()]
+            last_counts[:] = counts
             rpk, rln, n = timed("exchange", dexchange, spk, sln, counts, stride, out=recv_bufs)
         else:
             rpk, rln, n = spk, sln, step_pk
@@ -595,6 +599,33 @@ def main():
         except (OSError, ValueError, KeyError):
             traffic = None
 
+    # achievable HBM on this device beside the 8 TB/s peak: a plain copy of this
+    # rank's source events (1 GiB) into the arena with e2sar_hip_copy_spans (16-byte
+    # non-temporal loads and stores, one 16-KiB piece per workgroup), HIP events around 5 copies
+    copy_gbps = None
+    if not spread:
+        nb = min(src.numel(), R.arena_bytes) & ~255
+        span = [(src.data_ptr(), R.arena_ptr, nb)]
+        for _ in range(2):
+            ctx.copy_spans(span)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(5):
+            ctx.copy_spans(span)
+        c1.record()
+        torch.cuda.synchronize()
+        copy_gbps = 2 * nb * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+
+    # spread landing: the exchange's bytes against the xGMI links: this rank's
+    # datagram slots + lengths sent to other ranks per step / the exchange's time
+    xgmi = None
+    if spread and world > 1 and "exchange" in avg:
+        sent = sum(c for j, c in enumerate(last_counts) if j != rank) * (stride + 4)
+        xgmi = {"bytes_sent_per_step": sent, "exchange_ms": round(avg["exchange"], 5),
+                "achieved": round(sent / (avg["exchange"] * 1e-3) / 1e9, 1), "peak": XGMI_PEAK_GBS,
+                "unit": "GB/s", "frac": round(sent / (avg["exchange"] * 1e-3) / 1e9 / XGMI_PEAK_GBS, 4),
+                "backend": backend}
+
     total_payload = E * B * world * K
     value = total_payload / elapsed / 2**30
     step_bytes = E * (4 * B + 72 * npk)
@@ -723,7 +754,11 @@ def main():
                 "launches_per_step": {k: len(v) // max(1, args.roofline_steps) for k, v in per.items()},
                 "algorithmic_bytes_per_launch": int(launch_bytes),
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
+                "copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
+                "copy_what": "1 GiB device-to-device copy on this GPU (e2sar_hip_copy_spans), read + write bytes",
+                "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
             },
+            "xgmi": xgmi,
             "reas_cold": cold,
             "cpu_baseline": cpu,
         }

@@ -40,6 +40,14 @@ class SegEvent(C.Structure):
     ]
 
 
+class CopySpan(C.Structure):
+    _fields_ = [
+        ("src", C.c_uint64),
+        ("dst", C.c_uint64),
+        ("bytes", C.c_uint64),
+    ]
+
+
 class SegReasBatch(C.Structure):
     _fields_ = [
         ("d_events", C.c_uint64),

@@ -1482,33 +1482,48 @@ __global__ __launch_bounds__(kBlock) void zero_words_kernel(uint32_t *p, uint64_
 // Gather copy: blockIdx.y = span; 16-byte loads and stores when both ends are 16-byte
 // aligned (arena event buffers are 256-aligned; callers lay destinations out 64-aligned),
 // bytes otherwise and for the tail.
+// One workgroup copies one 16-KiB piece of one span (blockIdx.y): every thread issues its
+// four 16-byte non-temporal loads before any store, as seg_kernel does, so a large span
+// streams at the plain-copy rate (the bench's HBM calibration copies 1 GiB with it).
+constexpr uint32_t kCopyPiece = (uint32_t)kBlock * 16u * 4u;
 __global__ __launch_bounds__(kBlock) void copy_spans_kernel(CopySpans cs)
 {
     if (blockIdx.y >= cs.n) return;
     const CopySpan sp = cs.s[blockIdx.y];
+    const uint64_t base = (uint64_t)blockIdx.x * kCopyPiece;
+    if (base >= sp.bytes) return;
     const uint8_t *src = reinterpret_cast<const uint8_t *>(sp.src);
     uint8_t *dst = reinterpret_cast<uint8_t *>(sp.dst);
-    const uint64_t stride = (uint64_t)gridDim.x * kBlock;
-    uint64_t whole = 0;
+    const uint64_t end = (base + kCopyPiece < sp.bytes) ? base + kCopyPiece : sp.bytes;
+    uint64_t b0 = base;
     if (((sp.src | sp.dst) & 15u) == 0) {
-        whole = sp.bytes & ~15ull;
-        for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; 16 * i < whole; i += stride)
-            *reinterpret_cast<u32x4 *>(dst + 16 * i) = *reinterpret_cast<const u32x4 *>(src + 16 * i);
+        const uint64_t whole = sp.bytes & ~15ull;
+        u32x4 x[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t i = base + 16ull * ((uint64_t)u * kBlock + threadIdx.x);
+            x[u] = (i + 16 <= whole) ? ld16_nt(src + i) : u32x4{0u, 0u, 0u, 0u};
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const uint64_t i = base + 16ull * ((uint64_t)u * kBlock + threadIdx.x);
+            if (i + 16 <= whole) st16_nt(dst + i, x[u]);
+        }
+        b0 = (whole > base) ? ((whole < end) ? whole : end) : base;
     }
-    for (uint64_t b = whole + (uint64_t)blockIdx.x * kBlock + threadIdx.x; b < sp.bytes; b += stride) dst[b] = src[b];
+    for (uint64_t b = b0 + threadIdx.x; b < end; b += kBlock) dst[b] = src[b];
 }
 
 hipError_t launch_copy_spans(const CopySpans &cs, uint64_t largest, hipStream_t stream)
 {
     if (cs.n == 0 || largest == 0) return hipSuccess;
-    const uint64_t per = (uint64_t)kBlock * 16 * 4;             // 4 chunks per thread per block
-    const uint32_t bx = (uint32_t)std::min<uint64_t>(1024, (largest + per - 1) / per);
-    hipLaunchKernelGGL(copy_spans_kernel, dim3(bx, cs.n), dim3(kBlock), 0, stream, cs);
+    const uint64_t bx = (largest + kCopyPiece - 1) / kCopyPiece;
+    if (bx > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(copy_spans_kernel, dim3((uint32_t)bx, cs.n), dim3(kBlock), 0, stream, cs);
     return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------------
-// GC / recycle// ---------------------------------------------------------------------------------
 // GC / recycle
 
 __global__ __launch_bounds__(kBlock) void reas_gc_kernel(ReasDev R, uint64_t now, uint64_t timeout)

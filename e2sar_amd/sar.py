@@ -62,6 +62,14 @@ class Context:
     def sync(self) -> None:
         check(lib().e2sar_hip_ctx_sync(self._h))
 
+    def copy_spans(self, spans: Sequence[tuple], stream: Optional[torch.cuda.Stream] = None) -> None:
+        """(src_ptr, dst_ptr, nbytes) spans, device or pinned host memory, copied by
+        e2sar_hip_copy_spans (one launch per 64 spans)."""
+        arr = (_capi.CopySpan * max(1, len(spans)))()
+        for k, (a, b, n) in enumerate(spans):
+            arr[k] = _capi.CopySpan(int(a), int(b), int(n))
+        check(lib().e2sar_hip_copy_spans(self._h, arr, len(spans), C.c_void_p(_stream_handle(stream))))
+
     def close(self) -> None:
         if getattr(self, "_h", None) is not None and self._h.value:
             lib().e2sar_hip_ctx_destroy(self._h)

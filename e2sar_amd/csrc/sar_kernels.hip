@@ -42,9 +42,12 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_U
 #define E2SAR_REAS_U 4
 #endif
-#ifndef E2SAR_SEG_U
-#define E2SAR_SEG_U 4               // 16-byte output chunks per thread of seg_kernel
-#endif
+// seg_kernel's 16-byte output chunks per thread (U) is chosen per launch (launch_segment):
+// 8-KiB workgroups (U = 2) for events of up to 4 MiB of datagrams, 16-KiB (U = 4) above.
+// A/B (profiles/round2/ab2/segu*, suc3*, su9k): 205 x 1 MiB at MTU 1500, U = 2 1414-1422
+// GiB/s, 3 1414, 4 1399-1404, 6 1397, 8 1362, 1 1341; 1 MiB at MTU 9000, U = 2 1434 vs 4
+// 1418; 8 MiB at MTU 9000 (32 per launch), U = 2 1325-1334 vs 4 1362-1371.  E2SAR_SEG_U
+// (env, 2 or 4) overrides.
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
@@ -1635,20 +1638,32 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
     return hipGetLastError();
 }
 
+static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
+{
+    const char *v = getenv(var);
+    if (!v) return dflt;
+    const long x = atol(v);
+    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
+}
+
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream, const uint32_t *d_count)
 {
-    constexpr int U = E2SAR_SEG_U;
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
     if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32
+    const uint32_t U = env_u32("E2SAR_SEG_U", chunks <= (1u << 18) ? 2u : 4u, 2, 4) == 2u ? 2u : 4u;
     const uint32_t bpe = cdiv(chunks, (uint64_t)kBlock * U);
     const uint64_t grid = (uint64_t)bpe * nEvents;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((seg_kernel<U>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
-                       maxPld, pkts, stride, lens, d_count);
+    if (U == 2)
+        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
+                           maxPld, pkts, stride, lens, d_count);
+    else
+        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
+                           maxPld, pkts, stride, lens, d_count);
     return hipGetLastError();
 }
 
@@ -1733,13 +1748,6 @@ static uint32_t occupancy_lds(const char *var)
     return (x > 0 && x <= 65536) ? (uint32_t)x : 0u;
 }
 
-static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
-{
-    const char *v = getenv(var);
-    if (!v) return dflt;
-    const long x = atol(v);
-    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
-}
 
 static uint32_t scatter_group_size(uint32_t stride)
 {

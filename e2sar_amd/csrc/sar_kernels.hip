@@ -51,6 +51,11 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_CHAIN_SEG_U
+// chained form: seg blocks of 16 KiB (8-KiB blocks, as seg_kernel uses for 1 MiB events,
+// made the chained launch 147 -> 158 us: twice the blocks at the reassembly occupancy)
+#define E2SAR_CHAIN_SEG_U 4
+#endif
 #ifndef E2SAR_SCATTER_NT_LOAD
 // split / pipelined scatter: non-temporal datagram loads.  These forms serve the receive
 // path, whose datagrams were not just written by this GPU: a batch read back cold takes
@@ -1161,7 +1166,8 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(C
     const ChainBatch &B = cb.b[b];
     const uint32_t local = blockIdx.x - B.start;
     if (local < B.nSeg) {
-        seg_block<U, true>(B.events, B.bpe, lbVersion, maxPld, B.pkts, stride, B.lens, nullptr, local, B.G, B.tiles);
+        seg_block<E2SAR_CHAIN_SEG_U, true>(B.events, B.bpe, lbVersion, maxPld, B.pkts, stride, B.lens, nullptr, local,
+                                           B.G, B.tiles);
         return;
     }
     const uint32_t g = local - B.nSeg;
@@ -1836,7 +1842,7 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
         ChainBatch &B = cb.b[b];
         const uint64_t chunks = (uint64_t)B.maxPacketsPerEvent * (stride >> 4);
         if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-        B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * U) : 0u;
+        B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * E2SAR_CHAIN_SEG_U) : 0u;
         B.G = B.n ? reas_group_size(B.n, stride) : 1u;
         B.start = (uint32_t)grid;
         B.nSeg = B.bpe * B.nEvents;

@@ -54,8 +54,9 @@ struct e2sar_hip_reas {
     ReasDev alt{};                   // second slots + arena (COMPACTABLE), same ctl/lists
     void *stateMem = nullptr;        // slots | ctl | shards | completed | lost
     void *altSlots = nullptr;
-    // reference-order mode: sort keys / records / rocPRIM storage, and the PktInfo/FinishRec
-    // work buffer of reassemble_batch (both grow on demand)
+    // reference-order mode: sort keys / records / rocPRIM storage; and the PktInfo/FinishRec
+    // work buffer of reassemble_batch (reference order, or batches above kFusedMaxBytes);
+    // both grow on demand
     void *roScratch = nullptr;
     size_t roScratchBytes = 0;
     void *roWork = nullptr;
@@ -67,6 +68,10 @@ struct e2sar_hip_reas {
 };
 
 static bool ref_order(const e2sar_hip_reas *r) { return (r->cfg.flags & E2SAR_HIP_REAS_REFERENCE_ORDER) != 0; }
+
+// reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
+// that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
+static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 
 // Grow a device buffer to at least `need` bytes (a quarter more, to amortise).  Waits for
 // the device first: kernels of earlier batches may still read the old buffer.
@@ -520,6 +525,23 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
                                           r->roScratch, r->roScratchBytes, s);
         if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s);
         if (e != hipSuccess) return hip_fail(e, "reference-order reassembly launch");
+        return E2SAR_HIP_OK;
+    }
+    // A batch whose datagrams cannot still be in the 256 MiB Infinity Cache (more than
+    // kFusedMaxBytes of slots) is read back from HBM whatever the caller did before, and
+    // there the split form -- classify, then one-round scatter workgroups with streaming
+    // loads -- is the faster one: 8 MiB events at MTU 9000, 70 per launch (65,730
+    // datagrams, BASELINE config 3): 1116 GiB/s fused vs 1302 split.  Internal work buffer,
+    // grown on first use (synchronous: make the first such call outside graph capture).
+    static const uint64_t splitAbove = [] {
+        const char *v = getenv("E2SAR_REAS_SPLIT_ABOVE");
+        return v ? (uint64_t)strtoull(v, nullptr, 10) : (uint64_t)kFusedMaxBytes;
+    }();
+    if ((uint64_t)nPackets * stride > splitAbove) {
+        HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
+        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s);
+        if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;
     }
     hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);

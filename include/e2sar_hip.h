@@ -232,6 +232,9 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
 /* Parse, validate, look up / create and scatter nPackets datagrams held at
  * d_packets + p*stride with lengths d_lens[p] (the full datagram length as recvfrom
  * returns it, cpp:321).  now_ms stamps firstSegment for new events (hpp:97).
+ * One fused launch for batches of up to 320 MiB of slots; above that (a batch that cannot
+ * sit in the Infinity Cache) classify + scatter launches through an internal work buffer,
+ * grown on first use (that first call synchronises the device).
  * Asynchronous on `stream` (NULL = the context stream). */
 int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,

@@ -288,7 +288,10 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 // once the block's stores are done, the block adds the number of index-space chunks it
 // covered in each reassembly group's range of datagrams to that group's counter
 // (tiles[slot / tileG]); a group starts when its counter reaches its slots x stride/16.
-template <int U, bool HO>
+#ifndef E2SAR_SEG_BLOCK
+#define E2SAR_SEG_BLOCK 256         // seg_kernel threads per workgroup (A/B knob)
+#endif
+template <int U, bool HO, int SB = kBlock>
 __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict__ events, uint32_t blocksPerEvent,
                                           int lbVersion, uint32_t maxPld, uint8_t *__restrict__ pkts, uint32_t stride,
                                           uint32_t *__restrict__ lens, const uint32_t *__restrict__ dCount,
@@ -304,7 +307,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
     const uint32_t npk = (bytes + maxPld - 1u) / maxPld;
     const uint32_t spc = stride >> 4;
     const uint32_t nch = npk * spc;
-    const uint32_t j0 = bx * (uint32_t)(kBlock * U);
+    const uint32_t j0 = bx * (uint32_t)(SB * U);
     if (j0 >= nch) return;
 
     HdrWords hw;
@@ -322,7 +325,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
     // ---- phase 1: one load per chunk ----
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t j = j0 + (uint32_t)u * kBlock + threadIdx.x;
+        const uint32_t j = j0 + (uint32_t)u * SB + threadIdx.x;
         jj[u] = 0xFFFFFFFFu;
         cc[u] = LL[u] = kk[u] = sh[u] = 0;
         rare[u] = false;
@@ -406,7 +409,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         __syncthreads();
         if (threadIdx.x < 64) {
-            const uint32_t j1 = (j0 + (uint32_t)(kBlock * U) < nch) ? j0 + (uint32_t)(kBlock * U) : nch;
+            const uint32_t j1 = (j0 + (uint32_t)(SB * U) < nch) ? j0 + (uint32_t)(SB * U) : nch;
             const uint64_t s0 = (uint64_t)ev.pktBase + j0 / spc, s1 = (uint64_t)ev.pktBase + (j1 - 1u) / spc;
             const uint64_t t0 = s0 / tileG, t1 = s1 / tileG;
             for (uint64_t t = t0 + (threadIdx.x & 63u); t <= t1; t += 64u) {
@@ -427,14 +430,14 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
 }
 
 template <int U>
-__global__ __launch_bounds__(kBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
-                                                     uint32_t blocksPerEvent, int lbVersion,
-                                                     uint32_t maxPld, uint8_t *__restrict__ pkts,
-                                                     uint32_t stride, uint32_t *__restrict__ lens,
-                                                     const uint32_t *__restrict__ dCount)
+__global__ __launch_bounds__(E2SAR_SEG_BLOCK) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
+                                                              uint32_t blocksPerEvent, int lbVersion,
+                                                              uint32_t maxPld, uint8_t *__restrict__ pkts,
+                                                              uint32_t stride, uint32_t *__restrict__ lens,
+                                                              const uint32_t *__restrict__ dCount)
 {
-    seg_block<U, false>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount, blockIdx.x, 1u,
-                        nullptr);
+    seg_block<U, false, E2SAR_SEG_BLOCK>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount,
+                                         blockIdx.x, 1u, nullptr);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1661,15 +1664,15 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
     if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32
     const uint32_t U = env_u32("E2SAR_SEG_U", chunks <= (1u << 18) ? 2u : 4u, 2, 4) == 2u ? 2u : 4u;
-    const uint32_t bpe = cdiv(chunks, (uint64_t)kBlock * U);
+    const uint32_t bpe = cdiv(chunks, (uint64_t)E2SAR_SEG_BLOCK * U);
     const uint64_t grid = (uint64_t)bpe * nEvents;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (U == 2)
-        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
-                           maxPld, pkts, stride, lens, d_count);
+        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, bpe,
+                           lbVersion, maxPld, pkts, stride, lens, d_count);
     else
-        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(kBlock), 0, stream, d_events, bpe, lbVersion,
-                           maxPld, pkts, stride, lens, d_count);
+        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, bpe,
+                           lbVersion, maxPld, pkts, stride, lens, d_count);
     return hipGetLastError();
 }
 

@@ -67,6 +67,9 @@ def parse(argv=None):
                          "in line; pipelined: one launch scatters batch b while other workgroups classify "
                          "batch b+1 (two datagram buffers, one stream); chained: segmentation and "
                          "reassembly of a batch in one launch (segment_reassemble_batch)")
+    ap.add_argument("--reference-order", action="store_true",
+                    help="reassemble with E2SAR_HIP_REAS_REFERENCE_ORDER (the reference's arrival-order rules: "
+                         "key pass, radix sort, per-key walk, scatter)")
     ap.add_argument("--chain-batches", type=int, default=1,
                     help="chained form: batches per launch (1-8; each batch its own datagram buffer)")
     ap.add_argument("--roofline-steps", type=int, default=2)
@@ -312,8 +315,12 @@ def main():
     table = 1
     while table < args.table_factor * E:
         table <<= 1
+    from e2sar_amd import _capi
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
-                              lost_capacity=1024, arena_bytes=E * ev_stride + 4096)
+                              lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
+                              flags=_capi.REAS_REFERENCE_ORDER if args.reference_order else 0)
+    if args.reference_order and args.reas != "fused":
+        raise SystemExit("--reference-order runs through reassemble_batch (--reas fused)")
 
     spread = args.landing == "spread"
     if spread:
@@ -357,7 +364,8 @@ def main():
 
     # reassemble_batch runs classify + scatter inside for batches above 320 MiB of slots
     # (e2sar_hip.h); the timing entry then covers both launches
-    fused_name = "reas_kernel" if max_batch_pk * stride <= (320 << 20) else "reassemble_batch_split"
+    fused_name = ("reassemble_batch_ro" if args.reference_order else
+                  "reas_kernel" if max_batch_pk * stride <= (320 << 20) else "reassemble_batch_split")
 
     def reassemble(pk, ln, n, k, stream=None):
         """The receive side of one batch: one fused launch, or classify + scatter."""
@@ -573,7 +581,7 @@ def main():
     launch_bytes = per_launch_events * (2 * B + 36 * npk)
     bw_kernels = [k for k in avg if k in ("seg_kernel", "reas_kernel", "reas_scatter_kernel",
                                           "reas_scatter_classify_kernel", "segreas_kernel",
-                                          "reassemble_batch_split")]
+                                          "reassemble_batch_split", "reassemble_batch_ro")]
     dom = max(bw_kernels, key=lambda k: sum(per[k]))      # most time in the step
     dom_ms = avg[dom]
     if spread and dom == "reas_kernel":
@@ -736,6 +744,8 @@ def main():
                 "launch": "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times",
                 "overlap": bool(args.overlap),
                 "reassembly": {"fused": ("reas_kernel per batch" if fused_name == "reas_kernel" else
+                                         "reassemble_batch per batch, REFERENCE_ORDER: key pass, radix sort, "
+                                         "per-key walk, scatter" if args.reference_order else
                                          "reassemble_batch per batch: classify + scatter launches inside "
                                          "(batch above 320 MiB of slots)"),
                                "split": "reas_classify_kernel + reas_scatter_kernel per batch",

@@ -17,7 +17,7 @@ size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots)
 {
     size_t tb = 0;
     if (ro_sort_keys(nullptr, tb, nullptr, nullptr, n, ro_sort_end_bit(tableSlots), nullptr) != hipSuccess) return 0;
-    return 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(tb);
+    return ro_fixed_bytes(n) + ro_align(tb);
 }
 
 }  // namespace e2sar_amd

@@ -1345,7 +1345,8 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
 //                    its key in the table (find_or_create<keyOnly>) and emit a sort key
 //                    slot << 32 | position and a 16-byte record {off, plen, blen, hl};
 //   ro_sort_keys   : rocPRIM radix sort of the keys (ro_sort.hip);
-//   ro_walk_kernel : one thread per key walks that key's datagrams in arrival order with the
+//   ro_starts_kernel: the first sorted position of every key;
+//   ro_walk_kernel : one wave per key walks that key's datagrams in arrival order with the
 //                    reference's rules, creating items (arena buffers) as it goes, and writes
 //                    the PktInfo / FinishRec work records of the split form;
 //   reas_scatter_kernel then moves the bytes and publishes the completions.
@@ -1356,8 +1357,10 @@ constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                                         const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
-                                                        unsigned long long *__restrict__ keys, RoRec *__restrict__ recs)
+                                                        unsigned long long *__restrict__ keys, RoRec *__restrict__ recs,
+                                                        uint32_t *__restrict__ nStarts)
 {
+    if (blockIdx.x == 0 && threadIdx.x == 0) *nStarts = 0u;     // counted by ro_starts_kernel
     const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t p0 = wave * 64u;
@@ -1396,21 +1399,47 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     wave_stats(R, live, live ? raw.len : 0u, h.bad, h.derr, wave);
 }
 
-// One thread per sorted position; the first position of each key walks all of them.
-__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsigned long long *__restrict__ keys,
-                                                         const RoRec *__restrict__ recs, uint32_t n, uint64_t now,
-                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
+// Key starts: the first sorted position of every key that takes part goes to starts[] (in
+// any order, counted in *nStarts); positions that take no part get their empty work
+// record here.
+__global__ __launch_bounds__(kBlock) void ro_starts_kernel(const unsigned long long *__restrict__ keys,
+                                                           const RoRec *__restrict__ recs, uint32_t n,
+                                                           uint32_t tableSlots, PktInfo *__restrict__ info,
+                                                           uint32_t *__restrict__ starts, uint32_t *__restrict__ nStarts)
 {
     const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
     if (i >= n) return;
     const unsigned long long k = keys[i];
     const uint32_t slot = (uint32_t)(k >> 32);
-    if (slot >= R.tableSlots) {                                // takes no part: nothing to copy
+    if (slot >= tableSlots) {                                  // takes no part: nothing to copy
         const uint32_t q = (uint32_t)k;
         st16(reinterpret_cast<uint8_t *>(info + q), u32x4{0u, 0u, 0u, recs[q].hl});
         return;
     }
     if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == slot) return;   // not the key's first position
+    starts[atomicAdd(nStarts, 1u)] = i;
+}
+
+// One wave per key walks the key's datagrams in arrival order, 64 at a time, with the
+// reference's rules (cpp:361-427).  The item state (buffer, length, curBytes, fragments) is
+// wave-uniform.  Within a chunk the walk goes segment by segment: a segment starts where a
+// new item starts (offset 0, or no item in progress) and runs to the next offset-0 fragment;
+// a masked prefix sum of the payload lengths finds the first fragment whose add makes
+// curBytes equal the item's length (completion, cpp:403), which ends the segment early.
+// Fragments that overrun the item (made by a fragment with another bufferLength) count as
+// data errors and add nothing.  One segment per chunk is the usual case; duplicates, late
+// offset-0 fragments and replays after completion add segments.
+__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsigned long long *__restrict__ keys,
+                                                         const RoRec *__restrict__ recs, uint32_t n, uint64_t now,
+                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin,
+                                                         const uint32_t *__restrict__ starts,
+                                                         const uint32_t *__restrict__ nStarts)
+{
+    const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t lane = threadIdx.x & 63u;
+    if (w >= *nStarts) return;                                 // wave-uniform
+    const uint32_t s = starts[w];
+    const uint32_t slot = (uint32_t)(keys[s] >> 32);
     ReasSlot *sl = R.slots + slot;
     const uint64_t ev = sl->eventNum;
     const uint32_t d = sl->dataId;
@@ -1422,64 +1451,86 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
     uint64_t created = sl->created;
     long long live = 0;                                        // net change of items in progress
     uint32_t derr = 0;
-    for (uint32_t j = i; j < n; j++) {
-        const unsigned long long kj = keys[j];
-        if ((uint32_t)(kj >> 32) != slot) break;
+    for (uint32_t base = s;; base += 64u) {
+        const uint32_t j = base + lane;
+        const unsigned long long kj = (j < n) ? keys[j] : ~0ull;
+        const bool valid = (uint32_t)(kj >> 32) == slot;     // the key's positions are contiguous
+        const uint32_t nv = (uint32_t)__builtin_popcountll(__ballot(valid));
+        if (nv == 0u) break;
         const uint32_t q = (uint32_t)kj;
-        const RoRec rc = recs[q];
-        if (rc.off == 0u || !item) {
-            // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the one
-            // in progress in the map (cpp:361-369), which is dropped without a lost record
-            if (item) live--;
-            const uint64_t need = ((uint64_t)rc.blen + 255ull) & ~255ull;
-            boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
-            if (boff + rc.blen > R.arenaBytes) {
-                boff = kNoBuf;
-                atomicOr(&R.ctl->errorFlags, 2u);
+        RoRec rc = {0u, 0u, 0u, 0u};
+        if (valid) rc = recs[q];
+        for (uint32_t t = 0; t < nv;) {
+            if (!item || __shfl(rc.off, (int)t) == 0u) {
+                // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the
+                // one in progress (cpp:361-369), dropped without a lost record
+                if (item) live--;
+                const uint32_t blen = __shfl(rc.blen, (int)t);
+                const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
+                uint64_t nb = 0;
+                if (lane == 0) nb = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
+                nb = shfl_u64(nb, 0);
+                if (nb + blen > R.arenaBytes) {
+                    if (lane == 0) atomicOr(&R.ctl->errorFlags, 2u);
+                    nb = kNoBuf;
+                }
+                boff = nb;
+                ibytes = blen;
+                cur = 0;
+                frags = 0;
+                created = now;
+                item = true;
+                live++;
             }
-            ibytes = rc.blen;
-            cur = 0;
-            frags = 0;
-            created = now;
-            item = true;
-            live++;
+            const uint64_t zm = __ballot(valid && rc.off == 0u && lane > t);
+            const uint32_t v = zm ? (uint32_t)__builtin_ctzll(zm) : nv;      // next item start
+            const bool inseg = lane >= t && lane < v;
+            const bool viol = inseg && (uint64_t)rc.off + rc.plen > ibytes;
+            const uint32_t P = wave_incl_scan((inseg && !viol) ? rc.plen : 0u);
+            const uint64_t cm = __ballot(inseg && !viol && cur + P == (uint64_t)ibytes);
+            const uint32_t end = cm ? (uint32_t)__builtin_ctzll(cm) + 1u : v;
+            const bool inr = lane >= t && lane < end;
+            frags += (uint32_t)__builtin_popcountll(__ballot(inr && !viol));     // cpp:398-400
+            derr += (uint32_t)__builtin_popcountll(__ballot(inr && viol));
+            cur += (uint32_t)__builtin_amdgcn_readlane((int)P, (int)(end - 1u));
+            const bool comp = cm && lane == end - 1u;
+            if (inr) {
+                PktInfo pi{0ull, 0u, rc.hl};
+                if (!viol && boff != kNoBuf) {
+                    pi.dst = (uint64_t)(R.arena + boff + rc.off);
+                    pi.plen = rc.plen;
+                }
+                if (comp) {                                    // cpp:403: complete, erase, enqueue
+                    FinishRec f;
+                    f.ev = ev;
+                    f.boff = boff;
+                    f.slot = slot | kFinKeepSlot;
+                    f.bytes = ibytes;
+                    f.frags = frags;
+                    f.d = d;
+                    fin[q] = f;
+                    pi.hl |= kPktCompletes;
+                }
+                st16(reinterpret_cast<uint8_t *>(info + q), u32x4{(uint32_t)pi.dst, (uint32_t)(pi.dst >> 32), pi.plen, pi.hl});
+            }
+            if (cm) item = false;                              // inProgress-- in complete_event
+            t = end;
         }
-        PktInfo pi{0ull, 0u, rc.hl};
-        if ((uint64_t)rc.off + rc.plen > ibytes) {
-            derr++;                // the item was made by a fragment with another bufferLength
+        if (nv < 64u) break;
+    }
+    if (lane == 0) {
+        if (item) {
+            sl->bufOff = boff;
+            sl->bytes = ibytes;
+            sl->bvalid = 1u;
+            sl->acc = ((unsigned long long)frags << kAccFragShift) | (cur & kAccBytesMask);
+            sl->created = created;
         } else {
-            if (boff != kNoBuf) {
-                pi.dst = (uint64_t)(R.arena + boff + rc.off);
-                pi.plen = rc.plen;
-            }
-            frags++;                                           // cpp:398-400
-            cur += rc.plen;
-            if (cur == ibytes) {                               // cpp:403: complete, erase, enqueue
-                FinishRec f;
-                f.ev = ev;
-                f.boff = boff;
-                f.slot = slot | kFinKeepSlot;
-                f.bytes = ibytes;
-                f.frags = frags;
-                f.d = d;
-                fin[q] = f;
-                pi.hl |= kPktCompletes;
-                item = false;                                  // inProgress-- in complete_event
-            }
+            sl->state = kDone;                                 // no item left under this key
         }
-        st16(reinterpret_cast<uint8_t *>(info + q), u32x4{(uint32_t)pi.dst, (uint32_t)(pi.dst >> 32), pi.plen, pi.hl});
+        if (live) atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), (unsigned long long)live);
+        if (derr) atomicAdd(&R.shards[slot % kShards].dataErrCnt, (unsigned long long)derr);
     }
-    if (item) {
-        sl->bufOff = boff;
-        sl->bytes = ibytes;
-        sl->bvalid = 1u;
-        sl->acc = ((unsigned long long)frags << kAccFragShift) | (cur & kAccBytesMask);
-        sl->created = created;
-    } else {
-        sl->state = kDone;                                     // no item left under this key
-    }
-    if (live) atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), (unsigned long long)live);
-    if (derr) atomicAdd(&R.shards[slot % kShards].dataErrCnt, (unsigned long long)derr);
 }
 
 // Zero nWords dwords.  Used instead of hipMemsetAsync wherever the launch may be captured
@@ -1907,12 +1958,17 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     RoScratch sc = ro_scratch_layout(scratch, n);
     if (ro_scratch_bytes(n, R.tableSlots) > scratchBytes) return hipErrorInvalidValue;
     hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
-                       sc.keysIn, sc.recs);
+                       sc.keysIn, sc.recs, sc.nStarts);
     size_t tb = scratchBytes - (size_t)(sc.temp - static_cast<uint8_t *>(scratch));
     hipError_t e = ro_sort_keys(sc.temp, tb, sc.keysIn, sc.keysOut, n, ro_sort_end_bit(R.tableSlots), stream);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, sc.keysOut, sc.recs, n,
-                       now, reinterpret_cast<PktInfo *>(w), reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
+    PktInfo *info = reinterpret_cast<PktInfo *>(w);
+    hipLaunchKernelGGL(ro_starts_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, sc.keysOut, sc.recs, n,
+                       R.tableSlots, info, sc.starts, sc.nStarts);
+    // one wave per key: at most min(n, tableSlots) keys
+    const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
+    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc.keysOut, sc.recs,
+                       n, now, info, reinterpret_cast<FinishRec *>(w + work_fin_off(n)), sc.starts, sc.nStarts);
     return hipGetLastError();
 }
 

@@ -114,9 +114,11 @@ static_assert(sizeof(RoRec) == 16, "one dwordx4 per datagram");
 struct RoScratch {
     unsigned long long *keysIn, *keysOut;
     RoRec *recs;
+    uint32_t *starts, *nStarts;     // first sorted position of every key, and their count
     uint8_t *temp;
 };
 inline size_t ro_align(size_t x) { return (x + 255) & ~(size_t)255; }
+inline size_t ro_fixed_bytes(uint32_t n) { return 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(4ull * n) + 256; }
 inline RoScratch ro_scratch_layout(void *base, uint32_t n)
 {
     uint8_t *b = static_cast<uint8_t *>(base);
@@ -124,7 +126,9 @@ inline RoScratch ro_scratch_layout(void *base, uint32_t n)
     s.keysIn = reinterpret_cast<unsigned long long *>(b);
     s.keysOut = reinterpret_cast<unsigned long long *>(b + ro_align(8ull * n));
     s.recs = reinterpret_cast<RoRec *>(b + 2 * ro_align(8ull * n));
-    s.temp = b + 2 * ro_align(8ull * n) + ro_align(16ull * n);
+    s.starts = reinterpret_cast<uint32_t *>(b + 2 * ro_align(8ull * n) + ro_align(16ull * n));
+    s.nStarts = reinterpret_cast<uint32_t *>(b + 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(4ull * n));
+    s.temp = b + ro_fixed_bytes(n);
     return s;
 }
 // sort bits: slot (< tableSlots = 2^t) above the 32-bit position, plus the all-ones "no

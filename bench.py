@@ -648,6 +648,12 @@ def main():
     # Infinity Cache, so each launch reads its batch back from HBM) ----
     cold = None
     if args.cold_steps > 0 and not spread:
+        # a reassembler of its own, told its datagrams are cold (streaming loads in the
+        # scatter, E2SAR_HIP_REAS_COLD_DATAGRAMS); verify() and the steps below use it
+        R_hot = R
+        R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
+                                  lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
+                                  flags=_capi.REAS_COLD_DATAGRAMS)
         cb = args.cold_batch_events or args.batch_events
         cplans = plans if cb == args.batch_events else make_plans(cb)
         cbufs = [seg.alloc_packets(p.total_packets) for p in cplans]
@@ -710,8 +716,11 @@ def main():
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(c_ach / HBM_PEAK_GBS, 4),
                          "avg_launch_ms": round(c_ms, 5), "algorithmic_bytes_per_launch": int(c_bytes),
                          "all_launch_ms": {k: round(sum(v) / len(v), 5) for k, v in cper.items()}},
+            "flags": "E2SAR_HIP_REAS_COLD_DATAGRAMS",
         }
         del cbufs
+        R.close()
+        R = R_hot
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_seconds > 0:

@@ -74,6 +74,7 @@ class ReasConfig(C.Structure):
 
 REAS_COMPACTABLE = 1
 REAS_REFERENCE_ORDER = 2      # arrival-order rules of the reference receive body (e2sar_hip.h)
+REAS_COLD_DATAGRAMS = 4       # datagrams written long before: streaming loads in the scatter (e2sar_hip.h)
 
 
 class EventRec(C.Structure):

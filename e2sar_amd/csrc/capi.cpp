@@ -73,6 +73,13 @@ static bool ref_order(const e2sar_hip_reas *r) { return (r->cfg.flags & E2SAR_HI
 // that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
 static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 
+// Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
+// cold (E2SAR_HIP_REAS_COLD_DATAGRAMS), and for a batch too large to still be cached.
+static bool cold_loads(const e2sar_hip_reas *r, uint32_t n, uint32_t stride)
+{
+    return (r->cfg.flags & E2SAR_HIP_REAS_COLD_DATAGRAMS) != 0 || (uint64_t)n * stride > kFusedMaxBytes;
+}
+
 // Grow a device buffer to at least `need` bytes (a quarter more, to amortise).  Waits for
 // the device first: kernels of earlier batches may still read the old buffer.
 static hipError_t grow(void *&buf, size_t &have, size_t need)
@@ -525,7 +532,8 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
         HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
         hipError_t e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork,
                                           r->roScratch, r->roScratchBytes, s);
-        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s);
+        if (e == hipSuccess)
+            e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s, cold_loads(r, nPackets, stride));
         if (e != hipSuccess) return hip_fail(e, "reference-order reassembly launch");
         return E2SAR_HIP_OK;
     }
@@ -542,7 +550,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     if ((uint64_t)nPackets * stride > splitAbove) {
         HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
         hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork, s);
-        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s, true);
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;
     }
@@ -678,7 +686,7 @@ int e2sar_hip_reas_scatter(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    hipError_t e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, d_work, s);
+    hipError_t e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, d_work, s, cold_loads(r, nPackets, stride));
     if (e != hipSuccess) return hip_fail(e, "scatter launch");
     return E2SAR_HIP_OK;
 }
@@ -710,14 +718,15 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const ui
     if (ref_order(r)) {
         // arrival order needs the classification of b+1 after that of b, not inside the
         // scatter of b: two launches, same results
-        e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s);
+        e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s, cold_loads(r, sn, stride));
         if (e == hipSuccess && cn) {
             if (int rc = ro_prepare(r, cn)) return rc;
             e = launch_ro_classify(r->dev, d_cpk, stride, d_clens, cn, now_ms, d_cwork, r->roScratch,
                                    r->roScratchBytes, s);
         }
     } else {
-        e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms, d_cwork, s);
+        e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms, d_cwork, s,
+                                         cold_loads(r, sn, stride));
     }
     if (e != hipSuccess) return hip_fail(e, "scatter_classify launch");
     return E2SAR_HIP_OK;

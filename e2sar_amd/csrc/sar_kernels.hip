@@ -56,14 +56,11 @@ constexpr int kBlock = 256;
 // made the chained launch 147 -> 158 us: twice the blocks at the reassembly occupancy)
 #define E2SAR_CHAIN_SEG_U 4
 #endif
-#ifndef E2SAR_SCATTER_NT_LOAD
-// split / pipelined scatter: non-temporal datagram loads.  These forms serve the receive
-// path, whose datagrams were not just written by this GPU: a batch read back cold takes
-// 78.6 instead of 83.5 us (scatter) and 84.8 instead of 88.0 us (scatter + classify), and
-// the hot pipelined round trip gains too (profiles/round2/ab2).  The fused kernel keeps
-// default-policy loads: in the round trip they hit the Infinity Cache (nt: -10 %).
-#define E2SAR_SCATTER_NT_LOAD 1
-#endif
+// Split / pipelined scatter loads: non-temporal for datagrams that were written long before
+// (not in the Infinity Cache), plain for a batch just written -- chosen per launch
+// (launch_reas_scatter's nt; capi.cpp: E2SAR_HIP_REAS_COLD_DATAGRAMS, or a batch too large to
+// be cached).  Cold: a 205 x 1 MiB batch's scatter 85.1 (nt) vs 89.3 us (plain); hot: 68.0
+// (plain) vs 89.4 us (nt), reference-order batches 124.8 vs 148.1 us (profiles/round2/ab3/nt).
 #ifndef E2SAR_SCATTER_CHUNKS_PER_BLOCK
 #define E2SAR_SCATTER_CHUNKS_PER_BLOCK 1024u
 #endif
@@ -1227,7 +1224,7 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
 }
 
 // One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
-template <int U>
+template <int U, bool NT>
 __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                               uint32_t n, uint32_t G, const PktInfo *__restrict__ info,
                                               const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
@@ -1256,11 +1253,7 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
             else if ((p + 1u) * spc <= ic) p++;
             pp[u] = p;
             cc[u] = ic - p * spc;
-#if E2SAR_SCATTER_NT_LOAD
-            x[u] = ld16_nt(bpk + (uint64_t)p * stride + 16u * cc[u]);
-#else
-            x[u] = ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
-#endif
+            x[u] = NT ? ld16_nt(bpk + (uint64_t)p * stride + 16u * cc[u]) : ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
         }
     };
     issue(0);
@@ -1304,20 +1297,20 @@ __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const 
     classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t n, uint32_t G,
                                                               const PktInfo *__restrict__ info,
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    scatter_group<U>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+    scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
 // The classify workgroups have the low indices so they are dispatched first and their
 // round trips start while the scatter workgroups fill the machine.
-template <int U>
+template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
     const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
@@ -1330,7 +1323,7 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
                               blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
         return;
     }
-    scatter_group<U>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+    scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1949,29 +1942,39 @@ hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t 
 }
 
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
-                               const void *work, hipStream_t stream)
+                               const void *work, hipStream_t stream, bool nt)
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     const uint32_t G = scatter_group_size(stride);
-    hipLaunchKernelGGL((reas_scatter_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
-                       reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
+    if (nt)
+        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
+                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
+    else
+        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
+                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
 
 hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const uint8_t *spk, uint32_t sn,
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
-                                        uint64_t now, void *cwork, hipStream_t stream)
+                                        uint64_t now, void *cwork, hipStream_t stream, bool nt)
 {
     constexpr int U = E2SAR_REAS_U;
-    if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream);
+    if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream, nt);
     if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
     const uint8_t *sw = static_cast<const uint8_t *>(swork);
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     const uint32_t G = scatter_group_size(stride);
     const uint32_t nCls = cdiv(cn, kBlock);
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
+    if (nt)
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
+                       spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
+                       reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
+                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
+    else
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);

@@ -189,10 +189,10 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                                 uint32_t n, uint64_t now, void *work, hipStream_t stream);
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
-                               const void *work, hipStream_t stream);
+                               const void *work, hipStream_t stream, bool nt);   // nt: streaming datagram loads
 hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const uint8_t *spk, uint32_t sn,
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
-                                        uint64_t now, void *cwork, hipStream_t stream);
+                                        uint64_t now, void *cwork, hipStream_t stream, bool nt);
 hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream);   // p 4-byte aligned
 hipError_t launch_fill_bytes(void *p, int value, uint64_t n, hipStream_t stream); // any alignment
 hipError_t launch_gc(const ReasDev &R, uint64_t now, uint64_t timeout, hipStream_t stream);

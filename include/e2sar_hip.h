@@ -183,6 +183,12 @@ typedef struct e2sar_hip_reas_config {
  * synchronises the device, so capture a HIP graph only after a first batch of the largest
  * size has run). */
 #define E2SAR_HIP_REAS_REFERENCE_ORDER 2u
+/* The datagram batches of this reassembler were written long before they are reassembled
+ * (not in the Infinity Cache, e.g. received into HBM well ahead): the split, pipelined and
+ * reference-order forms read them with streaming (non-temporal) loads.  Without the flag
+ * they use cache-allocating loads (a batch just written -- by the segmenter, a copy, the NIC
+ * -- is read from cache), except for batches above 320 MiB of slots, which cannot be. */
+#define E2SAR_HIP_REAS_COLD_DATAGRAMS 4u
 
 /* Reassembled event handed to the caller (getEvent's out-params, cpp:626-641).
  * The bytes live at e2sar_hip_reas_arena() + arenaOffset until the arena is recycled. */

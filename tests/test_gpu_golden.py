@@ -122,12 +122,16 @@ def _expected(case):
     return {(e["eventNum"], e["dataId"]): e["hex"] for e in case["events"]}
 
 
-@pytest.mark.parametrize("mode", ["fused", "split"])
+@pytest.mark.parametrize("mode", ["fused", "split", "split_cold"])
 @pytest.mark.parametrize("per_datagram", [True, False])
 def test_golden_reassembly_cases(hip, golden, mode, per_datagram):
+    # split_cold: the split form with E2SAR_HIP_REAS_COLD_DATAGRAMS (streaming datagram loads)
+    from e2sar_amd import _capi
+    flags = _capi.REAS_COLD_DATAGRAMS if mode == "split_cold" else 0
+    mode = "split" if mode == "split_cold" else mode
     for case in golden["reassemble"]:
         name = case["name"]
-        got, st, lost = _reas_case(hip, case, mode, per_datagram)
+        got, st, lost = _reas_case(hip, case, mode, per_datagram, flags=flags)
         exp = case["stats"]
         if name == "mtu80_late_offset0_quirk_lb":
             # documented divergence of the default (order-insensitive) path, DESIGN.md 5.3:

@@ -1447,15 +1447,21 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
     uint64_t created = sl->created;
     long long live = 0;                                        // net change of items in progress
     uint32_t derr = 0;
+    // the next chunk's sort keys are loaded while this chunk is walked (one dependent round
+    // trip per chunk -- its records -- instead of two)
+    unsigned long long kn = (s + lane < n) ? keys[s + lane] : ~0ull;
     for (uint32_t base = s;; base += 64u) {
-        const uint32_t j = base + lane;
-        const unsigned long long kj = (j < n) ? keys[j] : ~0ull;
+        const unsigned long long kj = kn;
         const bool valid = (uint32_t)(kj >> 32) == slot;     // the key's positions are contiguous
         const uint32_t nv = (uint32_t)__builtin_popcountll(__ballot(valid));
         if (nv == 0u) break;
         const uint32_t q = (uint32_t)kj;
         RoRec rc = {0u, 0u, 0u, 0u};
         if (valid) rc = recs[q];
+        if (nv == 64u) {
+            const uint32_t jn = base + 64u + lane;
+            kn = (jn < n) ? keys[jn] : ~0ull;
+        }
         for (uint32_t t = 0; t < nv;) {
             if (!item || __shfl(rc.off, (int)t) == 0u) {
                 // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the

@@ -87,6 +87,10 @@ def parse(argv=None):
     ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="pipelined",
                     help="launch form of the cold leg (split: classify + scatter launches, timed apart; "
                          "pipelined: classify(0), then scatter(b) beside classify(b+1) in one launch)")
+    ap.add_argument("--subs", default="mtu9000,config3",
+                    help="sub-legs reported beside the headline at N=1 (comma list of mtu9000, config3; "
+                         "'none' to skip): north_star's MTU 9000 half (1 MiB events) and BASELINE config 3 "
+                         "(8 MiB events at MTU 9000, 70 events = 65,730 datagrams per launch)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -236,6 +240,55 @@ def graph_steps(args) -> int:
         return args.graph_steps
     return next(d for d in (4, 2, 1) if args.steps % d == 0)
 
+def _pmc_traffic(args, dom):
+    """HBM traffic per launch of kernel `dom` from the committed rocprofv3 PMC summaries
+    (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules) whose workload is this
+    one: profiles/pmc_latest.json and profiles/pmc_*.json."""
+    import glob
+    for path in [os.path.join(ROOT, "profiles", "pmc_latest.json")] + sorted(
+            glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
+        try:
+            with open(path) as f:
+                pmc = json.load(f)
+        except (OSError, ValueError):
+            continue
+        w = pmc.get("workload") or {}
+        if (w.get("mtu") == args.mtu and w.get("event_bytes") == args.event_bytes
+                and w.get("batch_events") == args.batch_events and w.get("lb_version", 2) == args.lb_version):
+            for k, v in (pmc.get("kernels") or {}).items():
+                if k.split("<")[0] == dom:
+                    return int(v["hbm_bytes_per_launch"]), pmc.get("file", os.path.relpath(path, ROOT))
+    return None, None
+
+
+def copy_calibration(ctx, torch, dev):
+    """Achievable HBM on this device beside the 8 TB/s peak: the best of
+    device copies with e2sar_hip_copy_spans (16-byte non-temporal loads and stores, one
+    16-KiB piece per workgroup) at 1 GiB and 4 GiB, read + write bytes per second, HIP
+    events around 5 copies each.  The larger copy amortises the launch's head and tail
+    (round 1's microbenchmark: 6.12 / 6.34 TB/s at 1 / 4 GiB), so the fraction of copy
+    the bench reports is taken against the best copy it measured, not a flattering one."""
+    best, per = 0.0, {}
+    for nb in (1 << 30, 4 << 30):
+        a = torch.empty(nb, dtype=torch.uint8, device=dev)
+        b = torch.empty(nb, dtype=torch.uint8, device=dev)
+        a.fill_(7)
+        span = [(a.data_ptr(), b.data_ptr(), nb)]
+        for _ in range(2):
+            ctx.copy_spans(span)
+        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        c0.record()
+        for _ in range(5):
+            ctx.copy_spans(span)
+        c1.record()
+        torch.cuda.synchronize()
+        g = 2 * nb * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+        per[f"{nb >> 30}GiB"] = round(g, 1)
+        best = max(best, g)
+        del a, b
+    torch.cuda.empty_cache()
+    return best, per
+
 
 def main():
     args = parse()
@@ -265,8 +318,54 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ctx = sar.Context(local)
-    coll_dev = dev if backend == "nccl" else torch.device("cpu")
+    env = Env(torch=torch, dist=dist, sar=sar, ctx=ctx, dev=dev, world=world, rank=rank, backend=backend,
+              coll_dev=dev if backend == "nccl" else torch.device("cpu"))
 
+    line = run_workload(args, env, headline=True)
+
+    # the other half of north_star's target and BASELINE config 3, in the same run: each a
+    # workload of its own (fresh buffers), its own roofline; `value` above stays config 2's
+    subs = [s for s in args.subs.split(",") if s and s != "none"] if world == 1 and args.landing == "own" else []
+    for name in subs:
+        over = SUB_LEGS[name]
+        a = argparse.Namespace(**{**vars(args), **over, "cold_steps": 0, "cpu_seconds": 0.0})
+        t0 = time.perf_counter()
+        sl = run_workload(a, env, headline=False)
+        torch.cuda.empty_cache()
+        if rank == 0:
+            line[name] = {
+                "workload": sl["config"]["workload"], "value": sl["value"], "unit": sl["unit"],
+                "ms_per_step": sl["ms_per_step"], "steps": sl["steps"], "verified": sl["config"]["verified_roundtrip"],
+                "reassembly": sl["config"]["reassembly"], "launch": sl["config"]["launch"],
+                "roofline": sl["roofline"], "leg_seconds": round(time.perf_counter() - t0, 1)}
+
+    if rank == 0 and world == 1 and args.cpu_seconds > 0:
+        line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+class Env:
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
+# sub-legs of the driver's default run (--subs): north_star's MTU 9000 half at 1 MiB, and
+# BASELINE config 3 (8 MiB events at MTU 9000, 70 events = 65,730 datagrams per launch)
+SUB_LEGS = {
+    "mtu9000": {"mtu": 9000},
+    "config3": {"mtu": 9000, "event_bytes": 8 << 20, "events": 280, "batch_events": 70},
+}
+
+
+def run_workload(args, env, headline: bool):
+    """One workload: inputs resident in HBM, warmup, a byte-exact round-trip check, the
+    timed steps (max over ranks), per-kernel HIP-event durations and the roofline.
+    Returns the JSON line (without cpu_baseline)."""
+    torch, dist, sar, ctx, dev = env.torch, env.dist, env.sar, env.ctx, env.dev
+    world, rank, backend, coll_dev = env.world, env.rank, env.backend, env.coll_dev
     B = args.event_bytes
     E = args.events
     seg = sar.DeviceSegmenter(ctx, mtu=args.mtu, lb_hdr_version=args.lb_version)
@@ -319,14 +418,20 @@ def main():
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
                               flags=_capi.REAS_REFERENCE_ORDER if args.reference_order else 0)
+    if args.landing == "spread":
+        R.set_owner(world, rank)          # reassemble only this rank's events (eventNum % world)
     if args.reference_order and args.reas != "fused":
         raise SystemExit("--reference-order runs through reassemble_batch (--reas fused)")
 
     spread = args.landing == "spread"
     if spread:
-        # every batch of the step lands in one buffer (contiguous), so one route and one
-        # all-to-all-v per step move it: one host read of the count matrix per step, which
-        # all_to_all_single needs for its split sizes
+        # every batch of the step lands in a region of one buffer; the datagrams this rank
+        # owns are reassembled where they land, batch by batch, while the batch is still in
+        # the Infinity Cache (the reassembler is set to this rank's ownership); then one route
+        # packs the step's FOREIGN datagrams per owner, one all-to-all-v moves them (split
+        # sizes from one all-gather of the count vectors: one host read per step), and the
+        # received datagrams -- cold by then -- are reassembled in the pipelined form with
+        # streaming loads
         from e2sar_amd.dist import PacketRouter, exchange as dexchange
         land = seg.alloc_packets(step_pk)
         land_off = [0]
@@ -336,6 +441,7 @@ def main():
         recv_cap = 2 * step_pk + 1024
         recv_bufs = (torch.empty(recv_cap * stride, dtype=torch.uint8, device=dev),
                      torch.empty(recv_cap, dtype=torch.int32, device=dev))
+        recv_work = [R.alloc_work(max_batch_pk) for _ in range(2)]
         if args.overlap or not args.eager or args.reas != "fused":
             log(args, "landing=spread: the exchange reads its split sizes on the host -> eager, fused, no overlap")
         args.overlap = False
@@ -377,22 +483,37 @@ def main():
             timed("reas_scatter_kernel", R.scatter, pk, stride, n, w, stream=stream)
 
     last_counts = []
+    last_recv = [0]
 
     def step_spread():
-        """Datagrams land on this rank whatever their owner: route by owner on the GPU, one
-        all-to-all-v over RCCL, reassemble what this rank owns."""
+        """Datagrams land on this rank whatever their owner: this rank's events are
+        reassembled in place (hot), the foreign ones routed, exchanged (RCCL all-to-all-v)
+        and reassembled by their owners."""
         lpk, lln = land
         for p, off in zip(plans, land_off):
             timed("seg_kernel", seg.segment, p, lpk[off * stride:], lln[off:])
-        spk, sln, cnt = timed("route_kernels", router.route, lpk, lln, step_pk)
+            timed("reas_kernel", R.reassemble, lpk[off * stride:], stride, lln[off:], p.total_packets)
+        spk, sln, cnt = timed("route_kernels", router.route, lpk, lln, step_pk, foreign_only=True)
         if world > 1:
-            counts = [int(c) for c in cnt.tolist()]
-            last_counts[:] = counts
-            rpk, rln, n = timed("exchange", dexchange, spk, sln, counts, stride, out=recv_bufs)
+            rpk, rln, n = timed("exchange", dexchange, spk, sln, cnt, stride, out=recv_bufs)
+            last_counts[:] = [int(c) for c in cnt.tolist()]
         else:
-            rpk, rln, n = spk, sln, step_pk
-        for c0 in range(0, n, max_batch_pk):
-            timed("reas_kernel", R.reassemble, rpk[c0 * stride:], stride, rln[c0:], min(max_batch_pk, n - c0))
+            last_counts[:] = [int(c) for c in cnt.tolist()]   # the step's one host read (nothing is foreign)
+            rpk, rln, n = spk, sln, 0
+        last_recv[0] = n
+        if n:
+            R.set_cold(True)
+            spans = [(c0, min(n, c0 + max_batch_pk)) for c0 in range(0, n, max_batch_pk)]
+            a0, b0 = spans[0]
+            timed("reas_classify_kernel", R.classify, rpk[a0 * stride:], stride, rln[a0:], b0 - a0, recv_work[0])
+            for k, (a, b) in enumerate(spans):
+                if k + 1 < len(spans):
+                    c, d = spans[k + 1]
+                    timed("reas_scatter_classify_kernel", R.scatter_classify, stride, rpk[a * stride:], b - a,
+                          recv_work[k % 2], rpk[c * stride:], rln[c:], d - c, recv_work[(k + 1) % 2])
+                else:
+                    timed("reas_scatter_kernel", R.scatter, rpk[a * stride:], stride, b - a, recv_work[k % 2])
+            R.set_cold(False)
 
     def step():
         """One step: recycle the event table/arena, then segment -> reassemble every batch.
@@ -585,54 +706,30 @@ def main():
     dom = max(bw_kernels, key=lambda k: sum(per[k]))      # most time in the step
     dom_ms = avg[dom]
     if spread and dom == "reas_kernel":
-        # the spread leg reassembles this rank's owned events in launches of max_batch_pk
-        # datagrams (the last one fewer): average algorithmic bytes per launch
-        owned = sum(1 for r in range(world) for i in range(E) if (r * E + i) % world == rank)
-        launch_bytes = owned * (2 * B + 36 * npk) / (len(per[dom]) / max(1, args.roofline_steps))
+        # the in-place launches reassemble the events that landed here AND are owned here
+        # (eventNum = rank * E + i): their payload, plus every landed datagram's 36-byte
+        # header read to find out (the foreign payloads are not loaded)
+        here = sum(1 for i in range(E) if (rank * E + i) % world == rank)
+        launch_bytes = (here * (2 * B) + E * 36 * npk) / len(plans)
     if dom == "segreas_kernel":
         launch_bytes *= 2                       # both stages' bytes in one launch: 4B + 72N per event
     achieved = launch_bytes / (dom_ms * 1e-3) / 1e9
 
     # HBM traffic per launch of the dominant kernel, from the committed rocprofv3 PMC passes
     # of this same workload (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules)
-    traffic = None
-    traffic_src = None
-    pmc_path = os.path.join(ROOT, "profiles", "pmc_latest.json")
-    if os.path.exists(pmc_path) and not spread:
-        try:
-            with open(pmc_path) as f:
-                pmc = json.load(f)
-            w = pmc.get("workload") or {}
-            if (w.get("mtu") == args.mtu and w.get("event_bytes") == B and w.get("batch_events") == args.batch_events
-                    and w.get("lb_version", 2) == args.lb_version):
-                for k, v in pmc["kernels"].items():
-                    if k.startswith(dom):
-                        traffic = int(v["hbm_bytes_per_launch"])
-                        traffic_src = pmc.get("file", "profiles/pmc_latest.json")
-        except (OSError, ValueError, KeyError):
-            traffic = None
+    traffic, traffic_src = (None, None) if (spread or args.reas != "fused" or args.overlap) else _pmc_traffic(args, dom)
 
     # achievable HBM on this device beside the 8 TB/s peak: a plain copy of this
     # rank's source events (1 GiB) into the arena with e2sar_hip_copy_spans (16-byte
     # non-temporal loads and stores, one 16-KiB piece per workgroup), HIP events around 5 copies
-    copy_gbps = None
-    if not spread:
-        nb = min(src.numel(), R.arena_bytes) & ~255
-        span = [(src.data_ptr(), R.arena_ptr, nb)]
-        for _ in range(2):
-            ctx.copy_spans(span)
-        c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        c0.record()
-        for _ in range(5):
-            ctx.copy_spans(span)
-        c1.record()
-        torch.cuda.synchronize()
-        copy_gbps = 2 * nb * 5 / (c0.elapsed_time(c1) * 1e-3) / 1e9
+    copy_gbps, copy_per = None, None
+    if headline and not spread:
+        copy_gbps, copy_per = copy_calibration(ctx, torch, dev)
 
     # spread landing: the exchange's bytes against the xGMI links: this rank's
     # datagram slots + lengths sent to other ranks per step / the exchange's time
     xgmi = None
-    if spread and world > 1 and "exchange" in avg:
+    if spread and world > 1 and "exchange" in avg and avg["exchange"] > 0:
         sent = sum(c for j, c in enumerate(last_counts) if j != rank) * (stride + 4)
         xgmi = {"bytes_sent_per_step": sent, "exchange_ms": round(avg["exchange"], 5),
                 "achieved": round(sent / (avg["exchange"] * 1e-3) / 1e9, 1), "peak": XGMI_PEAK_GBS,
@@ -722,11 +819,7 @@ def main():
         R.close()
         R = R_hot
 
-    cpu = None
-    if rank == 0 and world == 1 and args.cpu_seconds > 0:
-        cpu = cpu_baseline(args, args.cpu_seconds)
-
-    if rank == 0:
+    if True:
         line = {
             "metric": METRIC,
             "value": round(value, 3),
@@ -781,17 +874,19 @@ def main():
                 "algorithmic_bytes_per_launch": int(launch_bytes),
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
                 "copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
-                "copy_what": "1 GiB device-to-device copy on this GPU (e2sar_hip_copy_spans), read + write bytes",
+                "copy_what": ("best device-to-device copy on this GPU (e2sar_hip_copy_spans, 16-B non-temporal "
+                              "loads/stores) of 1 and 4 GiB, read + write bytes"),
+                "copy_GBps_by_size": copy_per,
                 "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
             },
             "xgmi": xgmi,
             "reas_cold": cold,
-            "cpu_baseline": cpu,
         }
-        print(json.dumps(line), flush=True)
-    if world > 1:
-        dist.destroy_process_group()
-
-
-if __name__ == "__main__":
-    main()
+        if spread:
+            line["spread"] = {"foreign_sent_per_step": sum(c for j, c in enumerate(last_counts) if j != rank),
+                              "received_per_step": last_recv[0], "route": "foreign only (e2sar_hip_route_foreign)",
+                              "in_place": "reas_kernel with e2sar_hip_reas_set_owner(world, rank)",
+                              "received_form": "reas_classify + reas_scatter_classify (pipelined, cold loads)"}
+    # free this workload's device buffers before the next one (sub-legs)
+    R.close()
+    return line

@@ -68,7 +68,7 @@ class ReasConfig(C.Structure):
         ("lostCapacity", C.c_uint32),
         ("arenaBytes", C.c_uint64),
         ("flags", C.c_uint32),
-        ("reserved", C.c_uint32),
+        ("groupSize", C.c_uint32),
     ]
 
 
@@ -183,6 +183,9 @@ SIGNATURES = {
     "e2sar_hip_reas_compact": (i, [vp, vp]),
     "e2sar_hip_route_workspace_bytes": (sz, [u32, u32]),
     "e2sar_hip_route_batch": (i, [vp, vp, u32, vp, u32, i, u32, u32, vp, vp, vp, vp, sz, vp]),
+    "e2sar_hip_route_foreign": (i, [vp, vp, u32, vp, u32, i, u32, u32, vp, vp, vp, vp, sz, vp]),
+    "e2sar_hip_reas_set_owner": (i, [vp, u32, u32]),
+    "e2sar_hip_reas_set_cold": (i, [vp, i]),
 }
 
 

@@ -411,6 +411,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     const uint32_t T = cfg->tableSlots;
     if (T < 64 || (T & (T - 1))) return fail(E2SAR_HIP_ERR_PARAMETER, "tableSlots must be a power of two >= 64");
     if (cfg->queueCapacity == 0 || cfg->lostCapacity == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "zero capacity");
+    if (cfg->groupSize > 64) return fail(E2SAR_HIP_ERR_PARAMETER, "groupSize must be 0 (auto) or 1..64");
     HIP_TRY(hipSetDevice(ctx->device));
     auto *r = new e2sar_hip_reas;
     r->ctx = ctx;
@@ -449,6 +450,9 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->dev.queueCapacity = cfg->queueCapacity;
     r->dev.lostCapacity = cfg->lostCapacity;
     r->dev.withLB = cfg->withLBHeader ? 1 : 0;
+    r->dev.ownWorld = 1;                       // every event is ours until set_owner
+    r->dev.ownSelf = 0;
+    r->dev.groupSize = cfg->groupSize;
     r->alt = r->dev;
     r->alt.arena = nullptr;
     if (cfg->flags & E2SAR_HIP_REAS_COMPACTABLE) {
@@ -543,11 +547,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     // loads -- is the faster one: 8 MiB events at MTU 9000, 70 per launch (65,730
     // datagrams, BASELINE config 3): 1116 GiB/s fused vs 1302 split.  Internal work buffer,
     // grown on first use (synchronous: make the first such call outside graph capture).
-    static const uint64_t splitAbove = [] {
-        const char *v = getenv("E2SAR_REAS_SPLIT_ABOVE");
-        return v ? (uint64_t)strtoull(v, nullptr, 10) : (uint64_t)kFusedMaxBytes;
-    }();
-    if ((uint64_t)nPackets * stride > splitAbove) {
+    if ((uint64_t)nPackets * stride > kFusedMaxBytes) {
         HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
         hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork, s);
         if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s, true);
@@ -905,10 +905,12 @@ size_t e2sar_hip_route_workspace_bytes(uint32_t nPackets, uint32_t world)
     return route_workspace_bytes(nPackets, world);
 }
 
-int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
-                          uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self, uint8_t *d_sendPackets,
-                          uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace, size_t workspaceBytes,
-                          void *stream)
+}  // extern "C"
+
+static int route(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
+                 uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self, int excludeSelf,
+                 uint8_t *d_sendPackets, uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
+                 size_t workspaceBytes, void *stream)
 {
     if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
     if (world == 0 || world > 64 || self >= world) return fail(E2SAR_HIP_ERR_PARAMETER, "world must be 1..64, self < world");
@@ -918,9 +920,48 @@ int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t
     if (workspaceBytes < route_workspace_bytes(nPackets, world)) return fail(E2SAR_HIP_ERR_PARAMETER, "workspace too small");
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    hipError_t e = launch_route(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, d_sendPackets,
-                                d_sendLens, d_counts, d_workspace, s);
+    hipError_t e = launch_route(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, excludeSelf,
+                                d_sendPackets, d_sendLens, d_counts, d_workspace, s);
     if (e != hipSuccess) return hip_fail(e, "route launch");
+    return E2SAR_HIP_OK;
+}
+
+extern "C" {
+
+int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
+                          uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self, uint8_t *d_sendPackets,
+                          uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace, size_t workspaceBytes,
+                          void *stream)
+{
+    return route(ctx, d_packets, stride, d_lens, nPackets, withLBHeader, world, self, 0, d_sendPackets, d_sendLens,
+                 d_counts, d_workspace, workspaceBytes, stream);
+}
+
+int e2sar_hip_route_foreign(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
+                            uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self,
+                            uint8_t *d_sendPackets, uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
+                            size_t workspaceBytes, void *stream)
+{
+    return route(ctx, d_packets, stride, d_lens, nPackets, withLBHeader, world, self, 1, d_sendPackets, d_sendLens,
+                 d_counts, d_workspace, workspaceBytes, stream);
+}
+
+int e2sar_hip_reas_set_owner(e2sar_hip_reas *r, uint32_t world, uint32_t self)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (world == 0 || world > 64 || self >= world) return fail(E2SAR_HIP_ERR_PARAMETER, "world must be 1..64, self < world");
+    std::lock_guard<std::mutex> lk(r->mu);
+    r->dev.ownWorld = r->alt.ownWorld = world;
+    r->dev.ownSelf = r->alt.ownSelf = self;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_set_cold(e2sar_hip_reas *r, int cold)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    std::lock_guard<std::mutex> lk(r->mu);
+    if (cold) r->cfg.flags |= E2SAR_HIP_REAS_COLD_DATAGRAMS;
+    else r->cfg.flags &= ~E2SAR_HIP_REAS_COLD_DATAGRAMS;
     return E2SAR_HIP_OK;
 }
 

@@ -1,16 +1,6 @@
-// ro_sort.hip -- the key sort of the reference-order reassembly mode (a radix sort of our own,
-// rocPRIM as an alternative),
-// in a translation unit of its own so the rocPRIM templates do not slow the main build.
-#include <algorithm>
-#include <cstdlib>
-#include <cstring>
-#include <rocprim/device/device_radix_sort.hpp>
-
+// ro_sort.hip -- the key sort of the reference-order reassembly mode: a stable radix sort
+// of our own on the slot bits of the sort keys.
 #include "sar_kernels.hpp"
-
-#ifndef E2SAR_RO_OWN_SORT_DEFAULT
-#define E2SAR_RO_OWN_SORT_DEFAULT 1
-#endif
 
 namespace e2sar_amd {
 
@@ -149,7 +139,7 @@ hipError_t slot_sort(void *temp, size_t &tempBytes, const unsigned long long *in
     }
     if (tempBytes < histB + totB + tmpB) return hipErrorInvalidValue;
     if (n == 0u) return hipSuccess;
-    if (passes == 0u) return hipMemcpyAsync(out, in, (size_t)8 * n, hipMemcpyDeviceToDevice, stream);
+    if (passes == 0u) return hipMemcpyAsync(out, in, (size_t)8 * n, hipMemcpyDeviceToDevice, stream);   // copy node: replays clean
     uint8_t *tb = static_cast<uint8_t *>(temp);
     uint32_t *hist = reinterpret_cast<uint32_t *>(tb);
     uint32_t *totals = reinterpret_cast<uint32_t *>(tb + histB);
@@ -177,37 +167,12 @@ hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long 
 {
     // keys are slot << 32 | position and arrive in position order; the sort is stable, so
     // sorting the slot bits alone (32 .. endBit) keeps each slot's positions in order.
-    // Default: the slot sort above -- 6 launches for 14 bits, 147.2 us per 205-event batch
-    // against 179.5 with rocPRIM's merge-sort form (9 launches) and 162.4 with its onesweep
-    // form, and a HIP graph can hold it.  E2SAR_RO_SORT=1 selects rocPRIM instead: onesweep
-    // outside graph capture, merge sort inside (onesweep memsets its look-back states, and a
-    // captured memset node writes garbage from the second replay on);
-    // E2SAR_RO_ONESWEEP: 0 never, 1 outside capture (default), 2 always (A/B only).
-    using Merge = rocprim::radix_sort_config<>;
-    using Onesweep = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
-                                                rocprim::default_config, 0>;
-    static const int onesweep = [] {      // 0 never, 1 outside capture, 2 always (A/B only)
-        const char *v = getenv("E2SAR_RO_ONESWEEP");
-        return v ? atoi(v) : 1;
-    }();
-    static const int own = [] {           // E2SAR_RO_SORT: 0 the slot sort above, 1 rocPRIM
-        const char *v = getenv("E2SAR_RO_SORT");
-        return v ? (atoi(v) == 0) : E2SAR_RO_OWN_SORT_DEFAULT;
-    }();
-    if (!temp) {            // size query: room for every form
-        size_t a = 0, b = 0, c = 0;
-        hipError_t e = rocprim::radix_sort_keys<Merge>(nullptr, a, in, out, (size_t)n, 32u, endBit, stream);
-        if (e == hipSuccess) e = rocprim::radix_sort_keys<Onesweep>(nullptr, b, in, out, (size_t)n, 32u, endBit, stream);
-        if (e == hipSuccess) e = slot_sort(nullptr, c, in, out, n, endBit, stream);
-        tempBytes = std::max(a, std::max(b, c));
-        return e;
-    }
-    if (own) return slot_sort(temp, tempBytes, in, out, n, endBit, stream);
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (onesweep == 2 ||
-        (onesweep == 1 && hipStreamIsCapturing(stream, &cs) == hipSuccess && cs == hipStreamCaptureStatusNone))
-        return rocprim::radix_sort_keys<Onesweep>(temp, tempBytes, in, out, (size_t)n, 32u, endBit, stream);
-    return rocprim::radix_sort_keys<Merge>(temp, tempBytes, in, out, (size_t)n, 32u, endBit, stream);
+    // The slot sort above: 6 launches for 14 bits, 147.2 us per 205-event batch against
+    // 179.5 with rocPRIM's merge-sort form (9 launches) and 162.4 with its onesweep form
+    // (round 2 A/B).  rocPRIM is not used: its onesweep form memsets look-back
+    // states, and a captured memset node writes garbage from the second replay on (DESIGN.md
+    // 4.4), so only a sort without memset nodes may run where a caller can capture.
+    return slot_sort(temp, tempBytes, in, out, n, endBit, stream);
 }
 
 size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots)

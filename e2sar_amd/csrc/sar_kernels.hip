@@ -666,6 +666,14 @@ __device__ __forceinline__ RawHdr load_hdr(const ReasDev &R, const uint8_t *__re
     return h;
 }
 
+// True for an event another rank owns (ReasDev.ownWorld > 1; owner = eventNum % world, the
+// key e2sarDPReassembler.hpp:224-229 steers receive threads by).  The modulo runs only when
+// ownership is set (a uniform branch).
+__device__ __forceinline__ bool foreign_event(const ReasDev &R, uint64_t ev)
+{
+    return R.ownWorld > 1u && (uint32_t)(ev % R.ownWorld) != R.ownSelf;
+}
+
 // Per-packet counters of one wave (cpp:331-357): one atomic per wave per counter, sharded.
 // Whole wave active.
 __device__ __forceinline__ void wave_stats(const ReasDev &R, bool live, uint32_t len, bool bad, bool derr,
@@ -737,7 +745,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
 
-    const uint32_t len = live ? raw.len : 0u;
+    uint32_t len = live ? raw.len : 0u;
     bool ok = false, bad = false, derr = false;
     uint64_t ev = 0;
     uint32_t d = 0, off = 0, blen = 0, pl = 0;
@@ -756,6 +764,13 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
             pl = len - hl;
             ok = true;
         }
+    }
+    if (ok && foreign_event(R, ev)) {                         // another rank's event: not ours
+        live = false;
+        ok = false;
+        len = 0;
+        ev = 0;
+        d = off = blen = pl = 0;
     }
 
     // ---- runs of equal keys ----
@@ -1012,7 +1027,10 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     };
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
     const uint32_t gPhase = bswap32(raw.re.y) & 15u;
-    const uint32_t gPlen = (raw.len >= hl) ? ((raw.len < stride) ? raw.len : stride) - hl : 0u;
+    uint32_t gPlen = (raw.len >= hl) ? ((raw.len < stride) ? raw.len : stride) - hl : 0u;
+    if (R.ownWorld > 1u && re_valid(raw.re.x) &&
+        foreign_event(R, ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4)))
+        gPlen = 0u;                                                    // another rank's: no payload loads
     auto issue = [&](uint32_t r0, u32x4(&xs)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -1367,6 +1385,8 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     const RawHdr raw = load_hdr(R, pkts, stride, lens, p);
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
     ParsedHdr h = parse_hdr(raw, hl, stride, live);
+    const bool foreign = h.ok && foreign_event(R, h.ev);      // another rank's event: takes no part
+    if (foreign) h = ParsedHdr{0, 0, 0, 0, 0, false, false, false};
     // bounds against the fragment's own bufferLength, before the lookup (the reference
     // memcpy's unchecked at cpp:391; dropped and counted here)
     if (h.ok && (uint64_t)h.off + h.pl > h.blen) {
@@ -1392,7 +1412,7 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         const u32x4 v = {h.off, h.pl, h.blen, hl};
         st16(reinterpret_cast<uint8_t *>(recs + p), v);
     }
-    wave_stats(R, live, live ? raw.len : 0u, h.bad, h.derr, wave);
+    wave_stats(R, live && !foreign, (live && !foreign) ? raw.len : 0u, h.bad, h.derr, wave);
 }
 
 // Key starts: the first sorted position of every key that takes part goes to starts[] (in
@@ -1726,13 +1746,25 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
     return hipGetLastError();
 }
 
-static uint32_t env_u32(const char *var, uint32_t dflt, uint32_t lo, uint32_t hi)
-{
-    const char *v = getenv(var);
-    if (!v) return dflt;
-    const long x = atol(v);
-    return (x >= (long)lo && x <= (long)hi) ? (uint32_t)x : dflt;
-}
+// Launch geometry is fixed at build time: the A/B knobs of earlier rounds are -D flags
+// (tools/build_variants.sh), never environment variables read by the shipped library.
+#ifndef E2SAR_SEG_U
+#define E2SAR_SEG_U 0               // seg_kernel 16-byte chunks per thread: 0 = auto (2 up to 4 MiB of datagrams, else 4)
+#endif
+#ifndef E2SAR_SCATTER_G
+#define E2SAR_SCATTER_G 0           // datagrams per scatter workgroup: 0 = auto (E2SAR_SCATTER_CHUNKS_PER_BLOCK)
+#endif
+#ifndef E2SAR_REAS_BALANCE
+#define E2SAR_REAS_BALANCE 1        // balance reas_kernel groups to whole residency waves
+#endif
+#ifndef E2SAR_SCATTER_LDS
+#define E2SAR_SCATTER_LDS 0         // dynamic LDS per scatter workgroup (occupancy cap); 0 = none
+#endif
+#ifndef E2SAR_PIPE_LDS
+#define E2SAR_PIPE_LDS 0            // same for the pipelined scatter+classify grid
+#endif
+static_assert(E2SAR_SEG_U == 0 || E2SAR_SEG_U == 2 || E2SAR_SEG_U == 4, "seg_kernel is built for U = 2 or 4");
+static_assert(E2SAR_SCATTER_G <= 64 && E2SAR_SCATTER_LDS <= 65536 && E2SAR_PIPE_LDS <= 65536, "knob out of range");
 
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
@@ -1742,7 +1774,7 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
     if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32
-    const uint32_t U = env_u32("E2SAR_SEG_U", chunks <= (1u << 18) ? 2u : 4u, 2, 4) == 2u ? 2u : 4u;
+    const uint32_t U = E2SAR_SEG_U ? (uint32_t)E2SAR_SEG_U : (chunks <= (1u << 18) ? 2u : 4u);
     const uint32_t bpe = cdiv(chunks, (uint64_t)E2SAR_SEG_BLOCK * U);
     const uint64_t grid = (uint64_t)bpe * nEvents;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
@@ -1826,15 +1858,9 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
     return hipGetLastError();
 }
 
-// Dynamic LDS requested only to cap workgroups per CU (A/B knob, default 0 = no cap):
-// fewer bytes in flight shorten the queueing latency that dependent table round trips see.
-static uint32_t occupancy_lds(const char *var)
-{
-    const char *v = getenv(var);
-    if (!v) return 0;
-    const long x = atol(v);
-    return (x > 0 && x <= 65536) ? (uint32_t)x : 0u;
-}
+// Dynamic LDS requested only to cap workgroups per CU (build knobs E2SAR_SCATTER_LDS /
+// E2SAR_PIPE_LDS, default 0 = no cap): fewer bytes in flight shorten the queueing latency
+// that dependent table round trips see.
 
 
 static uint32_t scatter_group_size(uint32_t stride)
@@ -1847,7 +1873,7 @@ static uint32_t scatter_group_size(uint32_t stride)
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
     while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK) G >>= 1;
-    return env_u32("E2SAR_SCATTER_G", G, 1, 64);       // A/B knob: exact datagrams per workgroup
+    return E2SAR_SCATTER_G ? (uint32_t)E2SAR_SCATTER_G : G;   // build knob: exact datagrams per workgroup
 }
 
 
@@ -1869,14 +1895,16 @@ static uint32_t reas_resident_groups()
     return c;
 }
 
-static uint32_t reas_group_size(uint32_t n, uint32_t stride)
+// fixedG: the reassembler's configured group size (e2sar_hip_reas_config.groupSize), 0 = auto
+static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG)
 {
+    if (fixedG) return fixedG < 64u ? fixedG : 64u;
     constexpr int U = E2SAR_REAS_U;
     // datagrams per workgroup: at most E2SAR_REAS_CHUNKS 16-byte chunks (A/B knob), <= 64.
     // (A/B: at MTU 1500 2K-chunk groups lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
     // 8 MiB events 4K chunks (4 datagrams per group) lose 27 % to 9K-18K: per-event counter
     // and table traffic grows with groups per event)
-    const uint32_t spc = stride >> 4, budget = env_u32("E2SAR_REAS_CHUNKS", E2SAR_REAS_CHUNKS_PER_BLOCK, 64, 1u << 20);
+    const uint32_t spc = stride >> 4, budget = E2SAR_REAS_CHUNKS_PER_BLOCK;
     uint32_t G = 64;
     while (G > 1 && G * spc > budget) G >>= 1;
     // Balance the launch over whole residency waves: with ceil(n/G) workgroups = 1.5 x
@@ -1887,7 +1915,7 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride)
     // workgroups on each event's table slot and counter (8 MiB events at MTU 9000 lose
     // 9 % at G 16 -> 10). 205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
     // reas_kernel 79.0 -> 77.6 us.
-    if (env_u32("E2SAR_REAS_BALANCE", 1, 0, 1)) {
+    if (E2SAR_REAS_BALANCE) {
         const uint32_t cap = reas_resident_groups<U>();
         if (cap) {
             const uint32_t G0 = G, waves = cdiv(cdiv(n, G0), cap);
@@ -1901,7 +1929,7 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride)
             G = best;
         }
     }
-    return env_u32("E2SAR_REAS_G", G, 1, 64);          // A/B knob: exact datagrams per workgroup
+    return G;
 }
 
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
@@ -1909,7 +1937,7 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
-    const uint32_t G = reas_group_size(n, stride);
+    const uint32_t G = reas_group_size(n, stride, R.groupSize);
     hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G);
     return hipGetLastError();
 }
@@ -1925,7 +1953,7 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
         const uint64_t chunks = (uint64_t)B.maxPacketsPerEvent * (stride >> 4);
         if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
         B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * E2SAR_CHAIN_SEG_U) : 0u;
-        B.G = B.n ? reas_group_size(B.n, stride) : 1u;
+        B.G = B.n ? reas_group_size(B.n, stride, R.groupSize) : 1u;
         B.start = (uint32_t)grid;
         B.nSeg = B.bpe * B.nEvents;
         grid += (uint64_t)B.nSeg + (B.n ? cdiv(B.n, B.G) : 0u);
@@ -1955,10 +1983,10 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const uint8_t *w = static_cast<const uint8_t *>(work);
     const uint32_t G = scatter_group_size(stride);
     if (nt)
-        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
+        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
                            reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     else
-        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(cdiv(n, G)), dim3(kBlock), occupancy_lds("E2SAR_SCATTER_LDS"), stream, R, pkts, stride, n, G,
+        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
                            reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
@@ -1975,12 +2003,12 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     const uint32_t G = scatter_group_size(stride);
     const uint32_t nCls = cdiv(cn, kBlock);
     if (nt)
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
     else
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), occupancy_lds("E2SAR_PIPE_LDS"), stream, R, stride,
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
@@ -2057,17 +2085,31 @@ __device__ __forceinline__ uint32_t route_dest(const uint8_t *pkts, uint32_t str
     return (uint32_t)(ev % world);
 }
 
+constexpr uint32_t kNoDest = 0xFFFFFFFFu;
+
+// Destination of datagram p, or kNoDest past the batch and -- foreign-only routing
+// (excludeSelf) -- for every datagram that stays here (owned here, or unparsable): those
+// are reassembled where they landed by a reassembler set to this rank's ownership.
+__device__ __forceinline__ uint32_t route_dest_x(const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                                 uint32_t p, uint32_t n, int withLB, uint32_t world, uint32_t self,
+                                                 int excludeSelf)
+{
+    if (p >= n) return kNoDest;
+    const uint32_t d = route_dest(pkts, stride, lens, p, withLB, world, self);
+    return (excludeSelf && d == self) ? kNoDest : d;
+}
+
 // per-block, per-destination counts (wave ballots, deterministic)
 __global__ __launch_bounds__(kBlock) void route_hist_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
                                                             const uint32_t *__restrict__ lens, uint32_t n, int withLB,
-                                                            uint32_t world, uint32_t self,
+                                                            uint32_t world, uint32_t self, int excludeSelf,
                                                             uint32_t *__restrict__ blockHist)
 {
     __shared__ uint32_t cnt[kMaxWorld];
     for (uint32_t d = threadIdx.x; d < world; d += kBlock) cnt[d] = 0;
     __syncthreads();
     const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
-    const uint32_t dest = (p < n) ? route_dest(pkts, stride, lens, p, withLB, world, self) : 0xFFFFFFFFu;
+    const uint32_t dest = route_dest_x(pkts, stride, lens, p, n, withLB, world, self, excludeSelf);
     for (uint32_t d = 0; d < world; d++) {
         const uint64_t m = __ballot(dest == d);
         if ((threadIdx.x & 63) == 0 && m) atomicAdd(&cnt[d], (uint32_t)__builtin_popcountll(m));
@@ -2138,7 +2180,7 @@ constexpr uint32_t kPackSplit = E2SAR_PACK_SPLIT;
 #endif
 __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
                                                             const uint32_t *__restrict__ lens, uint32_t n, int withLB,
-                                                            uint32_t world, uint32_t self,
+                                                            uint32_t world, uint32_t self, int excludeSelf,
                                                             const uint32_t *__restrict__ blockBase,
                                                             const uint32_t *__restrict__ destBase,
                                                             uint8_t *__restrict__ out, uint32_t *__restrict__ outLens)
@@ -2148,7 +2190,7 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
     const uint32_t g = blockIdx.x / kPackSplit, sl = blockIdx.x % kPackSplit;
     const uint32_t p = g * kBlock + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    const uint32_t dest = (p < n) ? route_dest(pkts, stride, lens, p, withLB, world, self) : 0xFFFFFFFFu;
+    const uint32_t dest = route_dest_x(pkts, stride, lens, p, n, withLB, world, self, excludeSelf);
     uint32_t rank = 0;
     for (uint32_t d = 0; d < world; d++) {
         const uint64_t m = __ballot(dest == d);
@@ -2156,14 +2198,16 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
         if (lane == 0) waveCnt[wv][d] = (uint32_t)__builtin_popcountll(m);
     }
     __syncthreads();
-    if (dest != 0xFFFFFFFFu) {
+    pos[threadIdx.x] = kNoDest;
+    if (dest != kNoDest) {
         uint32_t before = 0;
         for (uint32_t w = 0; w < wv; w++) before += waveCnt[w][dest];
         const uint32_t q = destBase[dest] + blockBase[(uint64_t)g * world + dest] + before + rank;
         pos[threadIdx.x] = q;
         if (sl == 0) outLens[q] = lens[p];
     }
-    __syncthreads();
+    // foreign-only routing leaves most blocks with nothing to move at small world sizes
+    if (!__syncthreads_or(dest != kNoDest)) return;
     const uint32_t p0 = g * kBlock;
     const uint32_t np = (n - p0 < kBlock) ? n - p0 : kBlock;
     const uint32_t spc = stride >> 4;
@@ -2175,7 +2219,7 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
     constexpr int UR = 4;
     for (uint32_t r0 = c0; r0 < c1; r0 += kBlock * UR) {
         u32x4 x[UR];
-        uint32_t kk[UR], cc[UR];
+        uint32_t qq[UR], cc[UR];
 #pragma unroll
         for (int u = 0; u < UR; u++) {
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
@@ -2183,16 +2227,17 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
             uint32_t k = (uint32_t)((float)ic * rspc);
             if (k * spc > ic) k--;
             else if ((k + 1u) * spc <= ic) k++;
-            kk[u] = k;
             cc[u] = ic - k * spc;
-            x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
-                                         : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+            qq[u] = (i < c1) ? pos[k] : kNoDest;                       // kNoDest: stays here
+            x[u] = u32x4{0u, 0u, 0u, 0u};
+            if (qq[u] != kNoDest)
+                x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
+                                             : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
         }
 #pragma unroll
         for (int u = 0; u < UR; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
-            if (i < c1) {
-                uint8_t *o = out + (uint64_t)pos[kk[u]] * stride + 16u * cc[u];
+            if (qq[u] != kNoDest) {
+                uint8_t *o = out + (uint64_t)qq[u] * stride + 16u * cc[u];
                 if (E2SAR_PACK_POL & 1) st16_nt(o, x[u]);
                 else st16(o, x[u]);
             }
@@ -2207,8 +2252,8 @@ size_t route_workspace_bytes(uint32_t n, uint32_t world)
 }
 
 hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
-                        uint32_t world, uint32_t self, uint8_t *out, uint32_t *outLens, uint32_t *counts,
-                        void *workspace, hipStream_t stream)
+                        uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
+                        uint32_t *counts, void *workspace, hipStream_t stream)
 {
     if (world == 0 || world > kMaxWorld || self >= world) return hipErrorInvalidValue;
     if (n == 0) return launch_zero_words(counts, world, stream);
@@ -2216,10 +2261,10 @@ hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *le
     uint32_t *blockHist = static_cast<uint32_t *>(workspace);
     uint32_t *destBase = blockHist + (size_t)nb * world;
     hipLaunchKernelGGL(route_hist_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
-                       self, blockHist);
+                       self, excludeSelf, blockHist);
     hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kBlock), 0, stream, blockHist, nb, world, counts, destBase);
     hipLaunchKernelGGL(route_pack_kernel, dim3(nb * kPackSplit), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
-                       self, blockHist, destBase, out, outLens);
+                       self, excludeSelf, blockHist, destBase, out, outLens);
     return hipGetLastError();
 }
 

@@ -78,6 +78,12 @@ struct ReasDev {
     uint32_t queueCapacity;
     uint32_t lostCapacity;
     int withLB;
+    // multi-GPU ownership (e2sar_hip_reas_set_owner): with ownWorld > 1 a datagram whose RE
+    // header parses but whose eventNum % ownWorld != ownSelf belongs to another rank and is
+    // skipped -- neither counted nor copied (that rank's reassembler counts it)
+    uint32_t ownWorld;
+    uint32_t ownSelf;
+    uint32_t groupSize;       // datagrams per reas_kernel workgroup (config), 0 = chip-balanced auto
 };
 
 // Per-datagram result of classification (held in LDS between the two phases of reas_kernel).
@@ -202,7 +208,7 @@ hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stre
 hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t stream);
 size_t route_workspace_bytes(uint32_t n, uint32_t world);
 hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
-                        uint32_t world, uint32_t self, uint8_t *out, uint32_t *outLens, uint32_t *counts,
-                        void *workspace, hipStream_t stream);
+                        uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
+                        uint32_t *counts, void *workspace, hipStream_t stream);
 
 }  // namespace e2sar_amd

@@ -207,11 +207,12 @@ class DeviceReassembler:
 
     def __init__(self, ctx: Context, with_lb_header: bool = False, table_slots: int = 4096,
                  queue_capacity: int = 4096, lost_capacity: int = 4096, arena_bytes: int = 1 << 30,
-                 compactable: bool = False, flags: int = 0):
+                 compactable: bool = False, flags: int = 0, group_size: int = 0):
+        """group_size: datagrams per fused-kernel workgroup (1..64), 0 = automatic."""
         self.ctx = ctx
         flags |= _capi.REAS_COMPACTABLE if compactable else 0
         cfg = _capi.ReasConfig(1 if with_lb_header else 0, table_slots, queue_capacity,
-                               lost_capacity, arena_bytes, flags, 0)
+                               lost_capacity, arena_bytes, flags, group_size)
         h = C.c_void_p()
         check(lib().e2sar_hip_reas_create(ctx.handle, C.byref(cfg), C.byref(h)))
         self._h = h
@@ -224,6 +225,14 @@ class DeviceReassembler:
     @property
     def handle(self):
         return self._h
+
+    def set_owner(self, world: int, rank: int) -> None:
+        """Take only events with eventNum % world == rank (e2sar_hip_reas_set_owner)."""
+        check(lib().e2sar_hip_reas_set_owner(self._h, int(world), int(rank)))
+
+    def set_cold(self, cold: bool) -> None:
+        """Streaming datagram loads for the following launches (e2sar_hip_reas_set_cold)."""
+        check(lib().e2sar_hip_reas_set_cold(self._h, 1 if cold else 0))
 
     def reassemble(self, packets: torch.Tensor, stride: int, lens: torch.Tensor, n: int,
                    now_ms: int = 0, stream: Optional[torch.cuda.Stream] = None) -> None:

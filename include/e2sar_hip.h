@@ -164,7 +164,9 @@ typedef struct e2sar_hip_reas_config {
     uint32_t lostCapacity;     /* lost-event records held until polled */
     uint64_t arenaBytes;       /* device arena that receives reassembled event bytes */
     uint32_t flags;            /* E2SAR_HIP_REAS_* */
-    uint32_t reserved;
+    uint32_t groupSize;        /* datagrams per workgroup of the fused reassembly kernel (1..64);
+                                  0 = automatic: a 9K-chunk budget balanced to whole residency
+                                  waves of the chip (the measured best) */
 } e2sar_hip_reas_config;
 
 /* Allocate a second table + arena so e2sar_hip_reas_compact() can move in-progress
@@ -377,6 +379,29 @@ int e2sar_hip_route_batch(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t
                           uint32_t world, uint32_t self, uint8_t *d_sendPackets,
                           uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
                           size_t workspaceBytes, void *stream);
+/* Foreign-only routing: as e2sar_hip_route_batch, but datagrams this rank keeps -- owned
+ * by `self`, or unparsable -- are neither packed nor counted (d_counts[self] = 0, and no
+ * byte of theirs is read beyond the RE header).  They are reassembled where they landed
+ * by a reassembler set to this rank's ownership (e2sar_hip_reas_set_owner), so only
+ * (world-1)/world of an evenly spread batch crosses HBM twice and xGMI once.  Asynchronous. */
+int e2sar_hip_route_foreign(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride,
+                            const uint32_t *d_lens, uint32_t nPackets, int withLBHeader,
+                            uint32_t world, uint32_t self, uint8_t *d_sendPackets,
+                            uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
+                            size_t workspaceBytes, void *stream);
+
+/* Ownership of a reassembler in a world of `world` ranks (1..64): from the next launch on,
+ * a datagram whose RE header parses but whose eventNum % world != self belongs to another
+ * rank and takes no part -- not counted in any statistic, no byte copied.  Unparsable
+ * datagrams are still counted (badHeaderDiscards) here.  world = 1 (the default) takes
+ * every datagram.  The receive-side counterpart of the reference's steering of every
+ * fragment of an event to one receiver by eventNum (e2sarDPReassembler.hpp:224-229). */
+int e2sar_hip_reas_set_owner(e2sar_hip_reas *r, uint32_t world, uint32_t self);
+/* Set (cold != 0) or clear E2SAR_HIP_REAS_COLD_DATAGRAMS for the following launches: a
+ * reassembler that takes both just-written and long-resident batches (e.g. datagrams
+ * reassembled where they landed, then datagrams received from other ranks) tells each
+ * launch how to load them. */
+int e2sar_hip_reas_set_cold(e2sar_hip_reas *r, int cold);
 
 #ifdef __cplusplus
 }

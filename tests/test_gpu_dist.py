@@ -1,11 +1,20 @@
-"""Config 4 on the HIP path: datagrams land spread over two ranks, are routed to their
-owner (eventNum % world) by the gfx950 route kernels, exchanged with
-e2sar_amd.dist.exchange, and reassembled by reas_kernel on the owner.
+"""Config 4 on the HIP path: datagrams land spread over the ranks, the owner of an event is
+eventNum % world, and every rank must end with exactly the events it owns.
 
-Both ranks share GPU 0 (the one-GPU rehearsal of the 8-GPU node) and talk over gloo, whose
-all-to-all stages through host memory; on the node the same code runs over RCCL.  Each
-rank's reassembled events and counters must equal the oracle's reassembly of the
-datagrams that rank received.
+Two forms of the receive side are checked, each rank's events and counters against the
+oracle's reassembly of the datagrams that rank processed:
+
+* ``all``: route every landed datagram to its owner (e2sar_hip_route_batch, self
+  included), one all-to-all-v, reassemble what arrived;
+* ``foreign`` (what bench.py's spread leg runs): reassemble the datagrams this rank owns
+  where they landed (e2sar_hip_reas_set_owner), route only the foreign ones
+  (e2sar_hip_route_foreign), exchange them (split sizes from one all-gather of the device
+  count vectors), reassemble what arrived.
+
+Two ranks share GPU 0 over gloo (all-to-all staged through host memory; RCCL refuses two
+ranks on one device).  The RCCL branch itself runs at world 1 in a fresh child process
+that initialises the ``nccl`` process group before any other GPU call: route -> exchange
+(device tensors through RCCL) -> reas_kernel, in both forms, against the oracle.
 """
 import os
 import socket
@@ -19,81 +28,143 @@ pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 
 
-def _worker(rank, world, port, result_q):
-    sys.path.insert(0, HERE)
-    sys.path.insert(0, os.path.dirname(HERE))
+def _spread_rank(rank, world, mode, corrupt=True):
+    """One rank's share of the spread-landing case; returns the fields the parent checks."""
     import torch
-    import torch.distributed as dist
 
     import oracle_ffi as O
     import sar_inputs as S
     from e2sar_amd import sar
     from e2sar_amd.dist import PacketRouter, exchange
 
-    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
-    try:
-        ctx = sar.Context(0)
-        mtu = 1500
-        sizes = [5000 + 7919 * i for i in range(10)] + [1, 1436, 1437]
-        evs = [S.event_bytes(100 + i, s) for i, s in enumerate(sizes)]
-        seg = sar.DeviceSegmenter(ctx, mtu=mtu, lb_hdr_version=2)
-        stride = seg.stride
-        # every rank segments the same events (deterministic); datagram k of the stream
-        # "lands" on rank k % world (a modelled NIC spread), so every multi-datagram event
-        # has fragments on both ranks
-        offs, cur = [], 0
-        for e in evs:
-            cur = (cur + 255) // 256 * 256
-            offs.append(cur)
-            cur += len(e)
-        host = np.zeros(cur, np.uint8)
-        for e, o in zip(evs, offs):
-            host[o:o + len(e)] = e
-        dsrc = torch.from_numpy(host).to(ctx.torch_device)
-        plan = seg.plan([(dsrc.data_ptr() + o, len(e), 100 + i, S.DATA_ID, S.entropy(i), S.lb_tick(i))
-                         for i, (e, o) in enumerate(zip(evs, offs))])
-        pk, ln = seg.alloc_packets(plan.total_packets)
-        seg.segment(plan, pk, ln)
-        n = plan.total_packets
-        landed = torch.arange(n, device=ctx.torch_device) % world == rank
-        lpk = pk[: n * stride].view(n, stride)[landed].contiguous().view(-1)
-        lln = ln[:n][landed].contiguous()
-        nl = int(landed.sum())
-        if rank == 1:
-            lpk[16] = 0x20                    # RE version 2: unparsable, stays on the landing rank
-        router = PacketRouter(ctx, stride, nl, world, rank)
+    ctx = sar.Context(0)
+    mtu = 1500
+    sizes = [5000 + 7919 * i for i in range(10)] + [1, 1436, 1437]
+    evs = [S.event_bytes(100 + i, s) for i, s in enumerate(sizes)]
+    seg = sar.DeviceSegmenter(ctx, mtu=mtu, lb_hdr_version=2)
+    stride = seg.stride
+    # every rank segments the same events (deterministic); datagram k of the stream
+    # "lands" on rank k % world (a modelled NIC spread), so every multi-datagram event
+    # has fragments on every rank
+    offs, cur = [], 0
+    for e in evs:
+        cur = (cur + 255) // 256 * 256
+        offs.append(cur)
+        cur += len(e)
+    host = np.zeros(cur, np.uint8)
+    for e, o in zip(evs, offs):
+        host[o:o + len(e)] = e
+    dsrc = torch.from_numpy(host).to(ctx.torch_device)
+    plan = seg.plan([(dsrc.data_ptr() + o, len(e), 100 + i, S.DATA_ID, S.entropy(i), S.lb_tick(i))
+                     for i, (e, o) in enumerate(zip(evs, offs))])
+    pk, ln = seg.alloc_packets(plan.total_packets)
+    seg.segment(plan, pk, ln)
+    n = plan.total_packets
+    landed = torch.arange(n, device=ctx.torch_device) % world == rank
+    lpk = pk[: n * stride].view(n, stride)[landed].contiguous().view(-1)
+    lln = ln[:n][landed].contiguous()
+    nl = int(landed.sum())
+    if corrupt and rank == world - 1:
+        lpk[16] = 0x20                    # RE version 2: unparsable, stays on the landing rank
+    router = PacketRouter(ctx, stride, nl, world, rank)
+    R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, arena_bytes=1 << 22)
+    hp_l = lpk[: nl * stride].view(nl, stride).cpu().numpy()
+    hl_l = lln[:nl].cpu().numpy().astype(np.uint32)
+    if mode == "foreign":
+        R.set_owner(world, rank)
+        R.reassemble(lpk, stride, lln, nl)                    # this rank's events, in place
+        spk, sln, cnt = router.route(lpk, lln, nl, foreign_only=True)
+        rpk, rln, nr = exchange(spk, sln, cnt, stride)       # device counts: one host read
+        counts = [int(c) for c in cnt.tolist()]
+        R.set_cold(True)
+        R.reassemble(rpk, stride, rln, nr)
+        # what this rank processed: the landed datagrams it keeps + what it received
+        keep = []
+        for k in range(nl):
+            ok, _, _, _, e, _ = O.re_parse(hp_l[k, 16:36].tobytes())
+            parsable = ok and 36 <= hl_l[k] <= stride
+            keep.append(not parsable or e % world == rank)
+        keep = np.array(keep, bool)
+    else:
         spk, sln, cnt = router.route(lpk, lln, nl)
         counts = [int(c) for c in cnt.tolist()]
         rpk, rln, nr = exchange(spk, sln, counts, stride)
-        R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, arena_bytes=1 << 22)
         R.reassemble(rpk, stride, rln, nr)
-        torch.cuda.synchronize()
-        got = {(r.eventNum, r.dataId): (R.event_bytes(r), r.numFragments) for r in R.poll()}
-        st = R.stats()
-        # oracle over the same received datagrams; offset 0 first per event (the device path
-        # is order-insensitive, the reference replaces an item on a late offset 0)
-        hp = rpk[: nr * stride].view(nr, stride).cpu().numpy()
-        hl = rln[:nr].cpu().numpy().astype(np.uint32)
-        key = [(int.from_bytes(hp[k, 28:36].tobytes(), "big"), int.from_bytes(hp[k, 20:24].tobytes(), "big"))
-               for k in range(nr)]
-        order = sorted(range(nr), key=lambda k: key[k])
-        ro = O.Reassembler(True)
+        keep = np.zeros(nl, bool)
+    torch.cuda.synchronize()
+    got = {(r.eventNum, r.dataId): (R.event_bytes(r), r.numFragments) for r in R.poll()}
+    st = R.stats()
+    hp_r = rpk[: nr * stride].view(nr, stride).cpu().numpy() if nr else np.zeros((0, stride), np.uint8)
+    hl_r = rln[:nr].cpu().numpy().astype(np.uint32) if nr else np.zeros(0, np.uint32)
+    hp = np.concatenate([hp_l[keep], hp_r])
+    hl = np.concatenate([hl_l[keep], hl_r])
+    # oracle over the same datagrams; offset 0 first per event (the device path is
+    # order-insensitive, the reference replaces an item on a late offset 0)
+    m = len(hl)
+    key = [(int.from_bytes(hp[k, 28:36].tobytes(), "big"), int.from_bytes(hp[k, 20:24].tobytes(), "big"))
+           for k in range(m)]
+    order = sorted(range(m), key=lambda k: key[k])
+    ro = O.Reassembler(True)
+    if m:
         ro.push_batch(hp[order], hl[order])
-        ref = {(e, d): b for b, e, d in ro.pop_all()}
-        rst = ro.stats()
-        mine = sorted(100 + i for i in range(len(sizes)) if (100 + i) % world == rank)
-        # the corrupted datagram is stream index 1 = event 100's second fragment: that event
-        # (owned by rank 0) stays in progress on both paths
-        complete = [e for e in mine if e != 100]
-        ok = sorted(e for e, _ in got) == sorted(e for e, _ in ref) == complete
-        ok = ok and all(got[k][0] == ref[k] for k in ref)
-        ok = ok and all(ref[(e, S.DATA_ID)] == evs[e - 100].tobytes() for e in complete)
-        fields = ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt", "inProgress")
-        stat_ok = {f: (int(getattr(st, f)), int(rst[f])) for f in fields}
-        ok = ok and all(a == b for a, b in stat_ok.values())
-        result_q.put((rank, ok, complete, counts, nr, stat_ok))
+    ref = {(e, d): b for b, e, d in ro.pop_all()}
+    rst = ro.stats()
+    mine = sorted(100 + i for i in range(len(sizes)) if (100 + i) % world == rank)
+    # the corrupted datagram is stream index world-1 (second fragment of event 100 at
+    # world 2): that event stays in progress on its owner
+    broken = {100} if (corrupt and world > 1) else set()
+    complete = [e for e in mine if e not in broken]
+    ok = sorted(e for e, _ in got) == sorted(e for e, _ in ref) == complete
+    ok = ok and all(got[k][0] == ref[k] for k in ref)
+    ok = ok and all(ref[(e, S.DATA_ID)] == evs[e - 100].tobytes() for e in complete)
+    fields = ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt", "inProgress")
+    stat_ok = {f: (int(getattr(st, f)), int(rst[f])) for f in fields}
+    ok = ok and all(a == b for a, b in stat_ok.values()) and st.errorFlags == 0
+    return rank, ok, complete, counts, nr, stat_ok
+
+
+def _gloo_worker(rank, world, port, mode, result_q):
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    import torch.distributed as dist
+    dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank, world_size=world)
+    try:
+        result_q.put(_spread_rank(rank, world, mode))
     finally:
         dist.destroy_process_group()
+
+
+def _nccl_worker(port, result_q):
+    """World 1 over RCCL: the process group is initialised (device_id given: eager RCCL
+    communicator) before any other GPU call of this fresh process."""
+    sys.path.insert(0, HERE)
+    sys.path.insert(0, os.path.dirname(HERE))
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    out = {}
+    try:
+        assert dist.get_backend() == "nccl"
+        # exchange() with host counts: one all_to_all_single of device tensors through RCCL
+        from e2sar_amd.dist import exchange
+        stride = 64
+        n = 1000
+        g = torch.Generator(device="cuda")
+        g.manual_seed(7)
+        spk = torch.randint(0, 256, (n * stride,), dtype=torch.uint8, device="cuda", generator=g)
+        sln = torch.randint(36, stride + 1, (n,), dtype=torch.int32, device="cuda", generator=g)
+        rpk, rln, nr = exchange(spk, sln, [n], stride)
+        out["raw"] = bool(nr == n and torch.equal(rpk[: n * stride], spk) and torch.equal(rln[:n], sln)
+                          and rpk.is_cuda)
+        for mode in ("all", "foreign"):
+            out[mode] = _spread_rank(0, 1, mode, corrupt=False)
+        out["backend"] = dist.get_backend()
+    finally:
+        dist.destroy_process_group()
+    result_q.put(out)
 
 
 def _free_port():
@@ -104,26 +175,53 @@ def _free_port():
     return p
 
 
-def test_spread_landing_route_exchange_reassemble_two_ranks():
+def _run(target, args, nproc, timeout=150):
     import torch.multiprocessing as mp
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
-    port = _free_port()
-    world = 2
-    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=a + (q,)) for a in args]
     for p in procs:
         p.start()
-    for p in procs:
-        p.join(timeout=100)
-    alive = [p for p in procs if p.is_alive()]
-    for p in alive:
-        p.kill()
+    res = []
+    try:
+        for _ in range(nproc):
+            res.append(q.get(timeout=timeout))
+    finally:
+        for p in procs:
+            p.join(timeout=30)
+        alive = [p for p in procs if p.is_alive()]
+        for p in alive:
+            p.kill()
     assert not alive, "rank processes hung"
-    res = sorted(q.get(timeout=5) for _ in range(world))
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+@pytest.mark.parametrize("mode", ["all", "foreign"])
+def test_spread_landing_route_exchange_reassemble_two_ranks(mode):
+    port = _free_port()
+    world = 2
+    res = sorted(_run(_gloo_worker, [(r, world, port, mode) for r in range(world)], world))
     for rank, ok, mine, counts, nr, stat_ok in res:
         assert ok, (rank, mine, counts, nr, stat_ok)
     # rank 1's unparsable datagram stayed home and was counted there; event 100 (owner rank
     # 0) misses that fragment
     assert res[1][5]["badHeaderDiscards"][0] == 1 and res[0][5]["badHeaderDiscards"][0] == 0
     assert res[0][5]["inProgress"] == (1, 1) and res[1][5]["inProgress"] == (0, 0)
-    assert all(p.exitcode == 0 for p in procs)
+    if mode == "foreign":
+        # nothing a rank owns is packed for itself
+        assert res[0][3][0] == 0 and res[1][3][1] == 0
+
+
+def test_rccl_exchange_world1_fresh_process():
+    """The nccl (RCCL) branch of dist.exchange on the GPU, route -> exchange -> reassemble."""
+    (out,) = _run(_nccl_worker, [(_free_port(),)], 1, timeout=240)
+    assert out["backend"] == "nccl"
+    assert out["raw"], "RCCL all-to-all of datagram slots changed bytes"
+    for mode in ("all", "foreign"):
+        rank, ok, mine, counts, nr, stat_ok = out[mode]
+        assert ok, (mode, mine, counts, nr, stat_ok)
+        assert mine == [100 + i for i in range(13)]
+    # route_batch sends every datagram to rank 0 through RCCL; foreign-only routing keeps them
+    assert out["all"][3] == [out["all"][4]] and out["all"][4] > 0
+    assert out["foreign"][3] == [0] and out["foreign"][4] == 0

@@ -147,7 +147,7 @@ def test_seg_generic_paths(hip):
 # reassembly parity
 
 
-def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096, mode="fused"):
+def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096, mode="fused", group_size=0):
     """Reassemble datagram rows pk[n, stride] (lens ln) on the GPU; returns ({(ev,d): bytes}, stats, reas).
 
     mode "fused": one reassemble_batch per batch; "split": classify every batch (in
@@ -161,7 +161,8 @@ def _reas_gpu(ctx, pk, ln, with_lb, batches=1, now=0, arena=1 << 28, table=4096,
     buf[:n, :stride] = pk
     dpk = _dev(buf.reshape(-1), ctx)
     dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), ctx)
-    R = sar.DeviceReassembler(ctx, with_lb_header=with_lb, table_slots=table, arena_bytes=arena)
+    R = sar.DeviceReassembler(ctx, with_lb_header=with_lb, table_slots=table, arena_bytes=arena,
+                              group_size=group_size)
     cuts = np.linspace(0, n, batches + 1).astype(int)
     spans = [(int(a), int(b)) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     if mode == "fused":
@@ -346,7 +347,7 @@ def test_reas_small_table_collisions(hip, reas_mode):
 
 
 @pytest.mark.parametrize("group", [1, 7, 33, 49, 63])
-def test_reas_group_sizes(hip, group, monkeypatch):
+def test_reas_group_sizes(hip, group):
     # datagrams per reassembly workgroup other than the power of two the chunk budget gives
     # (the launcher's wave balancing picks e.g. 49 at the bench's 205-event batches): groups
     # that cut through runs, events and the float chunk split, against the oracle
@@ -358,8 +359,7 @@ def test_reas_group_sizes(hip, group, monkeypatch):
     order = starts + rest              # offset 0 first, the rest shuffled
     pk, ln = pk[order], ln[order]
     ref, rst, _ = _reas_oracle(pk, ln, True)
-    monkeypatch.setenv("E2SAR_REAS_G", str(group))
-    got, st, _ = _reas_gpu(hip, pk, ln, True, batches=2, mode="fused")
+    got, st, _ = _reas_gpu(hip, pk, ln, True, batches=2, mode="fused", group_size=group)
     _check_reas(got, st, ref, rst)
     assert len(got) == 7 and st.errorFlags == 0
 
@@ -448,6 +448,103 @@ def test_reas_compaction_keeps_partial_events(hip):
         assert got[k] == b.tobytes()
     st = R.stats()
     assert st.eventSuccess == 6 and st.inProgress == 0 and st.arenaUsed < before.arenaUsed + 3 * 50176
+
+
+@pytest.mark.parametrize("mode", ["fused", "split", "pipelined", "reference_order"])
+def test_reas_owner_filter_takes_only_owned_events(hip, mode):
+    # e2sar_hip_reas_set_owner: a reassembler of rank r in a world of 3 reassembles exactly
+    # the events with eventNum % 3 == r and counts nothing of the others; unparsable
+    # datagrams are still counted where they are seen.  Oracle: the same batch restricted
+    # to the datagrams the rank keeps.
+    from e2sar_amd import _capi
+    world = 3
+    sizes = [70000, 1, 1437, 33333, 100000, 5000, 2873, 9000, 12345, 1436, 64000]
+    evs, pk, ln = _events_stream(len(sizes), sizes, 1500, seed=131)
+    starts = np.cumsum([0] + [O.num_packets(s, O.max_pld_len(1500)) for s in sizes])[:-1].tolist()
+    rest = [i for i in range(len(ln)) if i not in starts]
+    random.Random(17).shuffle(rest)
+    order = starts + rest
+    pk, ln = pk[order].copy(), ln[order].copy()
+    bad_ev = int.from_bytes(pk[len(ln) // 2, 28:36].tobytes(), "big")
+    pk[len(ln) // 2, 16] = 0x20                      # one unparsable datagram: its event never completes
+    keys = [O.re_parse(pk[k, 16:36].tobytes()) for k in range(len(ln))]
+    for r in range(world):
+        keep = np.array([not ok or e % world == r for ok, _, _, _, e, _ in keys], bool)
+        ref, rst, _ = _reas_oracle(pk[keep], ln[keep], True)
+        if mode == "reference_order":
+            from e2sar_amd import sar
+            torch = _torch()
+            n, stride = pk.shape
+            dpk = _dev(pk.reshape(-1), hip)
+            dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), hip)
+            R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=256, arena_bytes=1 << 24,
+                                      flags=_capi.REAS_REFERENCE_ORDER)
+            R.set_owner(world, r)
+            R.reassemble(dpk, stride, dln, n)
+            torch.cuda.synchronize()
+            got = {(x.eventNum, x.dataId): (R.event_bytes(x), x.numFragments) for x in R.poll()}
+            st = R.stats()
+        else:
+            got, st, R = _owner_reas(hip, pk, ln, world, r, mode)
+        _check_reas(got, st, ref, rst)
+        assert sorted(e for e, _ in got) == [k for k in range(len(sizes)) if k % world == r and k != bad_ev]
+        assert st.badHeaderDiscards == 1 and st.errorFlags == 0
+
+
+def _owner_reas(ctx, pk, ln, world, rank, mode):
+    from e2sar_amd import sar
+    torch = _torch()
+    n, stride = pk.shape
+    dpk = _dev(pk.reshape(-1), ctx)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), ctx)
+    R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, arena_bytes=1 << 24)
+    R.set_owner(world, rank)
+    cuts = [0, n // 3 + 1, 2 * n // 3 + 5, n]
+    spans = list(zip(cuts[:-1], cuts[1:]))
+    if mode == "fused":
+        for a, b in spans:
+            R.reassemble(dpk[a * stride:], stride, dln[a:], b - a)
+    elif mode == "split":
+        R.set_cold(True)
+        for a, b in spans:
+            w = R.alloc_work(b - a)
+            R.classify(dpk[a * stride:], stride, dln[a:], b - a, w)
+            R.scatter(dpk[a * stride:], stride, b - a, w)
+    else:
+        _pipelined(R, dpk, dln, stride, spans)
+    torch.cuda.synchronize()
+    got = {(x.eventNum, x.dataId): (R.event_bytes(x), x.numFragments) for x in R.poll()}
+    return got, R.stats(), R
+
+
+@pytest.mark.parametrize("world,self_rank", [(3, 0), (8, 5)])
+def test_route_foreign_skips_owned(hip, world, self_rank):
+    # foreign-only routing == the stable owner packing with this rank's share (and the
+    # unparsable datagram) left out; counts[self] == 0
+    from test_dist_gloo import stable_route
+    from e2sar_amd.dist import PacketRouter
+    evs, pk, ln = _events_stream(20, 7000, 1500, seed=83)
+    perm = np.random.default_rng(6).permutation(len(ln))
+    pk, ln = pk[perm].copy(), ln[perm].copy()
+    pk[3, 16] = 0x20
+    n, stride = pk.shape
+    dpk = _dev(pk.reshape(-1), hip)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), hip)
+    router = PacketRouter(hip, stride, n, world, self_rank)
+    spk, sln, cnt = router.route(dpk, dln, n, foreign_only=True)
+    _torch().cuda.synchronize()
+    rpk, rln, rcounts = stable_route(pk, ln, world, self_rank)
+    # drop this rank's span from the stable packing
+    base = sum(rcounts[:self_rank])
+    m = rcounts[self_rank]
+    rcounts = list(rcounts)
+    rcounts[self_rank] = 0
+    rpk = np.concatenate([rpk[:base], rpk[base + m:]])
+    rln = np.concatenate([rln[:base], rln[base + m:]])
+    assert cnt.cpu().tolist() == rcounts
+    k = len(rln)
+    np.testing.assert_array_equal(sln[:k].cpu().numpy().astype(np.uint32), rln)
+    np.testing.assert_array_equal(spk[: k * stride].cpu().numpy().reshape(k, stride), rpk)
 
 
 @pytest.mark.parametrize("world,self_rank", [(2, 1), (8, 3)])

@@ -890,3 +890,6 @@ def run_workload(args, env, headline: bool):
     # free this workload's device buffers before the next one (sub-legs)
     R.close()
     return line
+
+if __name__ == "__main__":
+    main()

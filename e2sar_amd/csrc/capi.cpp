@@ -10,6 +10,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <map>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -54,20 +55,56 @@ struct e2sar_hip_reas {
     ReasDev alt{};                   // second slots + arena (COMPACTABLE), same ctl/lists
     void *stateMem = nullptr;        // slots | ctl | shards | completed | lost
     void *altSlots = nullptr;
-    // reference-order mode: sort keys / records / rocPRIM storage; and the PktInfo/FinishRec
-    // work buffer of reassemble_batch (reference order, or batches above kFusedMaxBytes);
-    // both grow on demand
-    void *roScratch = nullptr;
-    size_t roScratchBytes = 0;
-    void *roWork = nullptr;
-    size_t roWorkBytes = 0;
-    // chained segment -> reassemble form: one ready counter per reassembly group
-    void *tiles = nullptr;
-    size_t tilesBytes = 0;
+    // Internal buffers, one set PER STREAM (two batches launched on different streams must
+    // not share work records or ready counters while both run): the reference-order sort
+    // keys / records / sort storage, the PktInfo/FinishRec work buffer of reassemble_batch
+    // (reference order, or batches above kFusedMaxBytes), the chained form's ready counters.
+    // They grow on demand, never inside a graph capture, and a buffer they outgrow is kept
+    // (retired) until the reassembler is destroyed: a graph captured before the growth still
+    // holds its address.
+    struct Scratch {
+        void *roScratch = nullptr;
+        size_t roScratchBytes = 0;
+        void *roWork = nullptr;
+        size_t roWorkBytes = 0;
+        void *tiles = nullptr;
+        size_t tilesBytes = 0;
+    };
+    std::map<hipStream_t, Scratch> scratch;
+    std::vector<void *> retired;
+    // one event per stream launched on outside capture: poll / lost_poll / get_stats wait
+    // for those launches only, not for the whole device
+    std::map<hipStream_t, hipEvent_t> done;
+    bool sawCapture = false;         // a launch was captured into a graph: snapshots wait for the device
     std::mutex mu;
 };
 
 static bool ref_order(const e2sar_hip_reas *r) { return (r->cfg.flags & E2SAR_HIP_REAS_REFERENCE_ORDER) != 0; }
+
+static bool capturing(hipStream_t s)
+{
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
+}
+
+// After a launch through this reassembler on stream s (caller holds r->mu): remember where
+// the stream is, so a later snapshot can wait for exactly these launches.
+static hipError_t note_launch(e2sar_hip_reas *r, hipStream_t s)
+{
+    if (capturing(s)) {
+        r->sawCapture = true;          // replays run wherever the caller puts them
+        return hipSuccess;
+    }
+    hipEvent_t &ev = r->done[s];
+    if (!ev) {
+        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
+        if (e != hipSuccess) {
+            r->done.erase(s);
+            return e;
+        }
+    }
+    return hipEventRecord(ev, s);
+}
 
 // reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
 // that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
@@ -80,32 +117,47 @@ static bool cold_loads(const e2sar_hip_reas *r, uint32_t n, uint32_t stride)
     return (r->cfg.flags & E2SAR_HIP_REAS_COLD_DATAGRAMS) != 0 || (uint64_t)n * stride > kFusedMaxBytes;
 }
 
-// Grow a device buffer to at least `need` bytes (a quarter more, to amortise).  Waits for
-// the device first: kernels of earlier batches may still read the old buffer.
-static hipError_t grow(void *&buf, size_t &have, size_t need)
+// Grow an internal buffer of stream s to at least `need` bytes (a quarter more, to
+// amortise); caller holds r->mu.  The old buffer is retired, not freed: kernels of earlier
+// batches may still read it, and a graph captured earlier holds its address.  Inside a
+// capture a buffer cannot grow (allocation there would break the capture): the call fails
+// with a LogicError naming the remedy instead.
+static int grow(e2sar_hip_reas *r, hipStream_t s, void *&buf, size_t &have, size_t need, bool *grew = nullptr)
 {
-    if (need <= have) return hipSuccess;
-    hipError_t e = hipDeviceSynchronize();
-    if (e != hipSuccess) return e;
-    if (buf) (void)hipFree(buf);
-    buf = nullptr;
-    have = 0;
+    if (grew) *grew = false;
+    if (need <= have) return E2SAR_HIP_OK;
+    if (capturing(s))
+        return fail(E2SAR_HIP_ERR_LOGIC, "an internal buffer must grow for this batch size inside a graph capture: "
+                                         "run one batch of the largest size on this stream before capturing");
     const size_t want = need + need / 4;
-    e = hipMalloc(&buf, want);
-    if (e != hipSuccess) {
-        buf = nullptr;
-        return e;
-    }
+    void *nb = nullptr;
+    hipError_t e = hipMalloc(&nb, want);
+    if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(internal buffer): ") + hipGetErrorString(e));
+    if (buf) r->retired.push_back(buf);
+    buf = nb;
     have = want;
-    return hipSuccess;
+    if (grew) *grew = true;
+    return E2SAR_HIP_OK;
+}
+
+static void free_internal(e2sar_hip_reas *r)
+{
+    for (auto &kv : r->scratch) {
+        if (kv.second.roScratch) (void)hipFree(kv.second.roScratch);
+        if (kv.second.roWork) (void)hipFree(kv.second.roWork);
+        if (kv.second.tiles) (void)hipFree(kv.second.tiles);
+    }
+    r->scratch.clear();
+    for (void *p : r->retired) (void)hipFree(p);
+    r->retired.clear();
+    for (auto &kv : r->done) (void)hipEventDestroy(kv.second);
+    r->done.clear();
 }
 
 // Free whatever a partly built reassembler holds (every pointer starts null).
 static void reas_release(e2sar_hip_reas *r)
 {
-    if (r->roScratch) (void)hipFree(r->roScratch);
-    if (r->roWork) (void)hipFree(r->roWork);
-    if (r->tiles) (void)hipFree(r->tiles);
+    free_internal(r);
     if (r->altSlots) (void)hipFree(r->altSlots);
     if (r->alt.arena && r->alt.arena != r->dev.arena) (void)hipFree(r->alt.arena);
     if (r->dev.arena) (void)hipFree(r->dev.arena);
@@ -496,9 +548,8 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     }
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
-    if (r->roScratch) (void)hipFree(r->roScratch);
-    if (r->roWork) (void)hipFree(r->roWork);
-    if (r->tiles) (void)hipFree(r->tiles);
+    (void)hipDeviceSynchronize();          // launches on other streams may still use the internal buffers
+    free_internal(r);
     delete r;
 }
 
@@ -506,13 +557,13 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r) { return r ? r->dev.arena : nul
 
 }  // extern "C"
 
-// Scratch of the reference-order classification for n datagrams (caller holds r->mu).
-static int ro_prepare(e2sar_hip_reas *r, uint32_t n)
+// Scratch of the reference-order classification for n datagrams on stream s (caller holds r->mu).
+static int ro_prepare(e2sar_hip_reas *r, hipStream_t s, uint32_t n)
 {
     const size_t need = ro_scratch_bytes(n, r->dev.tableSlots);
-    if (need == 0) return fail(E2SAR_HIP_ERR_SYSTEM, "rocPRIM sort storage query failed");
-    HIP_TRY(grow(r->roScratch, r->roScratchBytes, need));
-    return E2SAR_HIP_OK;
+    if (need == 0) return fail(E2SAR_HIP_ERR_SYSTEM, "sort storage query failed");
+    auto &sc = r->scratch[s];
+    return grow(r, s, sc.roScratch, sc.roScratchBytes, need);
 }
 
 extern "C" {
@@ -530,14 +581,16 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    auto &sc = r->scratch[s];
     if (ref_order(r)) {
         // classify in arrival order into the internal work buffer, then the scatter kernel
-        if (int rc = ro_prepare(r, nPackets)) return rc;
-        HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
-        hipError_t e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork,
-                                          r->roScratch, r->roScratchBytes, s);
+        if (int rc = ro_prepare(r, s, nPackets)) return rc;
+        if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, work_bytes(nPackets))) return rc;
+        hipError_t e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork,
+                                          sc.roScratch, sc.roScratchBytes, s);
         if (e == hipSuccess)
-            e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s, cold_loads(r, nPackets, stride));
+            e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, cold_loads(r, nPackets, stride));
+        if (e == hipSuccess) e = note_launch(r, s);
         if (e != hipSuccess) return hip_fail(e, "reference-order reassembly launch");
         return E2SAR_HIP_OK;
     }
@@ -545,16 +598,18 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     // kFusedMaxBytes of slots) is read back from HBM whatever the caller did before, and
     // there the split form -- classify, then one-round scatter workgroups with streaming
     // loads -- is the faster one: 8 MiB events at MTU 9000, 70 per launch (65,730
-    // datagrams, BASELINE config 3): 1116 GiB/s fused vs 1302 split.  Internal work buffer,
-    // grown on first use (synchronous: make the first such call outside graph capture).
+    // datagrams, BASELINE config 3): 1116 GiB/s fused vs 1302 split.  Internal work buffer
+    // of this stream, grown on first use (outside graph capture).
     if ((uint64_t)nPackets * stride > kFusedMaxBytes) {
-        HIP_TRY(grow(r->roWork, r->roWorkBytes, work_bytes(nPackets)));
-        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, r->roWork, s);
-        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, r->roWork, s, true);
+        if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, work_bytes(nPackets))) return rc;
+        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, true);
+        if (e == hipSuccess) e = note_launch(r, s);
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;
     }
     hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;
 }
@@ -595,13 +650,16 @@ static int segreas(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches, u
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    if (r->tilesBytes < 4ull * words) {
-        HIP_TRY(grow(r->tiles, r->tilesBytes, 4ull * words));
-        HIP_TRY(hipMemset(r->tiles, 0, r->tilesBytes));      // counters start at 0; each launch leaves them 0
-    }
+    auto &sc = r->scratch[s];
+    if (int rc = grow(r, s, sc.tiles, sc.tilesBytes, 4ull * words)) return rc;
     for (uint32_t b = 0; b < cb.nb; b++)
-        cb.b[b].tiles = static_cast<uint32_t *>(r->tiles) + reinterpret_cast<uintptr_t>(cb.b[b].tiles);
-    hipError_t e = launch_segreas(cb, lbHdrVersion, maxPldLen, stride, r->dev, now_ms, s);
+        cb.b[b].tiles = static_cast<uint32_t *>(sc.tiles) + reinterpret_cast<uintptr_t>(cb.b[b].tiles);
+    // the launch's ready counters start at 0: zeroed by a kernel (capture-safe)
+    // before every launch, so a group that gave up waiting in an earlier launch (error bit 4)
+    // cannot leave a count behind for this one
+    hipError_t e = launch_zero_words(sc.tiles, words, s);
+    if (e == hipSuccess) e = launch_segreas(cb, lbHdrVersion, maxPldLen, stride, r->dev, now_ms, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "segreas_kernel launch");
     return E2SAR_HIP_OK;
 }
@@ -634,6 +692,7 @@ int e2sar_hip_relay_plan(e2sar_hip_reas *r, uint32_t firstRecord, uint32_t maxEv
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     hipError_t e = launch_relay_plan(r->dev, firstRecord, maxEvents, (uint32_t)maxPldLen, lbTick, entropyBase,
                                      d_events, d_counts, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "relay_plan launch");
     return E2SAR_HIP_OK;
 }
@@ -664,12 +723,14 @@ int e2sar_hip_reas_classify(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     hipError_t e;
     if (ref_order(r)) {
-        if (int rc = ro_prepare(r, nPackets)) return rc;
-        e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, r->roScratch,
-                               r->roScratchBytes, s);
+        if (int rc = ro_prepare(r, s, nPackets)) return rc;
+        const auto &sc = r->scratch[s];
+        e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, sc.roScratch,
+                               sc.roScratchBytes, s);
     } else {
         e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, s);
     }
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "classify launch");
     return E2SAR_HIP_OK;
 }
@@ -687,6 +748,7 @@ int e2sar_hip_reas_scatter(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     hipError_t e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, d_work, s, cold_loads(r, nPackets, stride));
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "scatter launch");
     return E2SAR_HIP_OK;
 }
@@ -720,14 +782,16 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const ui
         // scatter of b: two launches, same results
         e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s, cold_loads(r, sn, stride));
         if (e == hipSuccess && cn) {
-            if (int rc = ro_prepare(r, cn)) return rc;
-            e = launch_ro_classify(r->dev, d_cpk, stride, d_clens, cn, now_ms, d_cwork, r->roScratch,
-                                   r->roScratchBytes, s);
+            if (int rc = ro_prepare(r, s, cn)) return rc;
+            const auto &sc = r->scratch[s];
+            e = launch_ro_classify(r->dev, d_cpk, stride, d_clens, cn, now_ms, d_cwork, sc.roScratch,
+                                   sc.roScratchBytes, s);
         }
     } else {
         e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms, d_cwork, s,
                                          cold_loads(r, sn, stride));
     }
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "scatter_classify launch");
     return E2SAR_HIP_OK;
 }
@@ -739,20 +803,34 @@ int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, v
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     hipError_t e = launch_gc(r->dev, now_ms, timeout_ms, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "gc launch");
     return E2SAR_HIP_OK;
 }
 
-// Snapshot of the control block.  Launches may run on any stream (reassemble_batch and the
-// split forms take the caller's stream), so the snapshot waits for the whole device, not
-// just the context stream: every kernel launched through this reassembler before the call
-// has finished, and r->mu (held by the caller) keeps new ones from starting, so the
-// read-modify-write of the list counts in poll / lost_poll cannot race a kernel's
-// completion atomics.
-static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
+// Wait until every kernel launched through this reassembler has finished (caller holds
+// r->mu, so no new one starts): the events recorded after each launch, one per stream used,
+// not the whole device -- other reassemblers, copy streams and unrelated work run on, and a
+// capture in progress on another thread is not disturbed.  Once a launch of this reassembler
+// has been captured into a graph, its replays can run on any stream, so the wait falls back
+// to the device.
+static int wait_launches(e2sar_hip_reas *r)
 {
     HIP_TRY(hipSetDevice(r->ctx->device));
-    HIP_TRY(hipDeviceSynchronize());
+    if (r->sawCapture) {
+        HIP_TRY(hipDeviceSynchronize());
+        return E2SAR_HIP_OK;
+    }
+    for (auto &kv : r->done) HIP_TRY(hipEventSynchronize(kv.second));
+    return E2SAR_HIP_OK;
+}
+
+// Snapshot of the control block after every launch of this reassembler finished
+// (wait_launches), so the read-modify-write of the list counts in poll / lost_poll cannot
+// race a kernel's completion atomics.
+static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
+{
+    if (int rc = wait_launches(r)) return rc;
     HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
     if (sum) {
         std::vector<ReasShard> sh(kShards);
@@ -853,12 +931,14 @@ int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream)
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     if (!force) {
         ReasCtl c;
+        if (int rc = wait_launches(r)) return rc;
         HIP_TRY(hipStreamSynchronize(s));
         HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
         if (c.inProgress != 0) return fail(E2SAR_HIP_ERR_LOGIC, "events still in progress");
         if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
     }
     hipError_t e = launch_recycle(r->dev, force != 0, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "recycle launch");
     return E2SAR_HIP_OK;
 }
@@ -871,10 +951,12 @@ int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream)
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
     ReasCtl c;
+    if (int rc = wait_launches(r)) return rc;
     HIP_TRY(hipStreamSynchronize(s));
     HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
     if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
     hipError_t e = launch_compact(r->dev, r->alt, s);
+    if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "compact launch");
     std::swap(r->dev.slots, r->alt.slots);
     std::swap(r->dev.arena, r->alt.arena);
@@ -897,6 +979,7 @@ int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream)
                               (offsetof(ReasCtl, inProgress) - offsetof(ReasCtl, eventSuccess)) / 4, s));
     HIP_TRY(launch_zero_words(r->dev.shards, sizeof(ReasShard) * kShards / 4, s));
     HIP_TRY(launch_zero_words(ctl + offsetof(ReasCtl, errorFlags), 1, s));
+    HIP_TRY(note_launch(r, s));
     return E2SAR_HIP_OK;
 }
 

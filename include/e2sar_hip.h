@@ -181,9 +181,9 @@ typedef struct e2sar_hip_reas_config {
  * order in the batch.  Without the flag the device path is order-insensitive: every
  * fragment joins its event and completion is tested per run of a launch (identical results
  * whenever offset 0 arrives first and there are no duplicates).  The mode
- * adds a key sort per batch and device scratch that grows on demand (a launch that grows it
- * synchronises the device, so capture a HIP graph only after a first batch of the largest
- * size has run). */
+ * adds a key sort per batch and device scratch that grows on demand (per stream; it cannot
+ * grow inside a graph capture -- such a launch fails with LOGIC -- so capture only after a
+ * first batch of the largest size has run on the capturing stream). */
 #define E2SAR_HIP_REAS_REFERENCE_ORDER 2u
 /* The datagram batches of this reassembler were written long before they are reassembled
  * (not in the Infinity Cache, e.g. received into HBM well ahead): the split, pipelined and
@@ -244,8 +244,12 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
  * d_packets + p*stride with lengths d_lens[p] (the full datagram length as recvfrom
  * returns it, cpp:321).  now_ms stamps firstSegment for new events (hpp:97).
  * One fused launch for batches of up to 320 MiB of slots; above that (a batch that cannot
- * sit in the Infinity Cache) classify + scatter launches through an internal work buffer,
- * grown on first use (that first call synchronises the device).
+ * sit in the Infinity Cache) classify + scatter launches through an internal work buffer.
+ * Internal buffers (this form, reference order, the chained form's counters) are kept
+ * per stream, so batches may be launched on several streams at once; they grow on first
+ * use for a size, never inside a graph capture (LOGIC error: run one batch of the largest
+ * size on the stream first), and an outgrown buffer stays allocated until destroy, so a
+ * graph captured earlier keeps valid addresses.
  * Asynchronous on `stream` (NULL = the context stream). */
 int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
@@ -280,16 +284,18 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride,
  * (reassemblyLoss, cpp:252-274).  Asynchronous. */
 int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, void *stream);
 
-/* Drain completed events.  Synchronises the device (every stream: launches may have used
- * any stream) under the reassembler's lock, so no kernel of this reassembler runs while
- * the list is drained.  Records are returned in completion order of the device;
- * *nOut <= cap.  Records beyond cap stay queued. */
+/* Drain completed events.  Waits, under the reassembler's lock, for every kernel launched
+ * through this reassembler (an event recorded after each launch on each stream used; other
+ * streams and reassemblers are not waited for), so none runs while the list is drained.
+ * Once a launch of this reassembler has been captured into a HIP graph, replays may run on
+ * any stream and the wait covers the whole device.  Records are returned in completion
+ * order of the device; *nOut <= cap.  Records beyond cap stay queued. */
 int e2sar_hip_reas_poll(e2sar_hip_reas *r, e2sar_hip_event_rec *out, uint32_t cap,
                         uint32_t *nOut);
-/* Drain lost-event records (synchronises the device, as reas_poll). */
+/* Drain lost-event records (waits for this reassembler's launches, as reas_poll). */
 int e2sar_hip_reas_lost_poll(e2sar_hip_reas *r, e2sar_hip_lost_rec *out, uint32_t cap,
                              uint32_t *nOut);
-/* Stats snapshot (synchronises the device, as reas_poll). */
+/* Stats snapshot (waits for this reassembler's launches, as reas_poll). */
 int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out);
 /* Recycle the arena and the event table.  Only legal when no event is in progress
  * and every completed record has been polled (else E2SAR_HIP_ERR_LOGIC); the caller

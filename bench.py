@@ -425,19 +425,16 @@ def run_workload(args, env, headline: bool):
 
     spread = args.landing == "spread"
     if spread:
-        # every batch of the step lands in a region of one buffer; the datagrams this rank
-        # owns are reassembled where they land, batch by batch, while the batch is still in
-        # the Infinity Cache (the reassembler is set to this rank's ownership); then one route
-        # packs the step's FOREIGN datagrams per owner, one all-to-all-v moves them (split
-        # sizes from one all-gather of the count vectors: one host read per step), and the
-        # received datagrams -- cold by then -- are reassembled in the pipelined form with
-        # streaming loads
-        from e2sar_amd.dist import PacketRouter, exchange as dexchange
-        land = seg.alloc_packets(step_pk)
-        land_off = [0]
-        for p in plans[:-1]:
-            land_off.append(land_off[-1] + p.total_packets)
-        router = PacketRouter(ctx, stride, step_pk, world, rank)
+        # each batch lands in one reused buffer (as the own-landing leg's); while it is still
+        # in the Infinity Cache the datagrams this rank owns are reassembled where they
+        # landed (the reassembler is set to this rank's ownership) and the FOREIGN ones are
+        # appended to per-owner regions (e2sar_hip_route_append); at the end of the step one
+        # all-to-all-v sends the regions (split sizes from one all-gather of the counters:
+        # one host read per step) and the received datagrams -- cold by then -- are
+        # reassembled in the pipelined form with streaming loads
+        from e2sar_amd.dist import RegionRouter
+        land = seg.alloc_packets(max_batch_pk)
+        router = RegionRouter(ctx, stride, step_pk, max_batch_pk, world, rank)
         recv_cap = 2 * step_pk + 1024
         recv_bufs = (torch.empty(recv_cap * stride, dtype=torch.uint8, device=dev),
                      torch.empty(recv_cap, dtype=torch.int32, device=dev))
@@ -490,16 +487,19 @@ def run_workload(args, env, headline: bool):
         reassembled in place (hot), the foreign ones routed, exchanged (RCCL all-to-all-v)
         and reassembled by their owners."""
         lpk, lln = land
-        for p, off in zip(plans, land_off):
-            timed("seg_kernel", seg.segment, p, lpk[off * stride:], lln[off:])
-            timed("reas_kernel", R.reassemble, lpk[off * stride:], stride, lln[off:], p.total_packets)
-        spk, sln, cnt = timed("route_kernels", router.route, lpk, lln, step_pk, foreign_only=True)
+        router.reset()
+        for p in plans:
+            timed("seg_kernel", seg.segment, p, lpk, lln)
+            timed("reas_kernel", R.reassemble, lpk, stride, lln, p.total_packets)
+            timed("route_kernels", router.route, lpk, lln, p.total_packets)
         if world > 1:
-            rpk, rln, n = timed("exchange", dexchange, spk, sln, cnt, stride, out=recv_bufs)
-            last_counts[:] = [int(c) for c in cnt.tolist()]
+            rpk, rln, n = timed("exchange", router.exchange, out=recv_bufs)
+            last_counts[:] = [int(c) for c in router.running.tolist()]
         else:
-            last_counts[:] = [int(c) for c in cnt.tolist()]   # the step's one host read (nothing is foreign)
-            rpk, rln, n = spk, sln, 0
+            last_counts[:] = [int(c) for c in router.running.tolist()]   # the step's one host read (nothing is foreign)
+            if last_counts[0]:
+                raise SystemExit("spread landing at N=1 routed a datagram away")
+            rpk, rln, n = recv_bufs[0], recv_bufs[1], 0
         last_recv[0] = n
         if n:
             R.set_cold(True)

@@ -11,6 +11,7 @@
 #include <cstring>
 #include <deque>
 #include <map>
+#include <set>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -72,9 +73,11 @@ struct e2sar_hip_reas {
     };
     std::map<hipStream_t, Scratch> scratch;
     std::vector<void *> retired;
-    // one event per stream launched on outside capture: poll / lost_poll / get_stats wait
-    // for those launches only, not for the whole device
-    std::map<hipStream_t, hipEvent_t> done;
+    // the streams launched on outside capture: poll / lost_poll / get_stats wait for those
+    // streams only, not for the whole device (an event recorded on each at snapshot time --
+    // not after every launch: a marker between kernels lengthens the next kernel's start)
+    std::set<hipStream_t> streams;
+    hipEvent_t waitEv = nullptr;
     bool sawCapture = false;         // a launch was captured into a graph: snapshots wait for the device
     std::mutex mu;
 };
@@ -87,23 +90,13 @@ static bool capturing(hipStream_t s)
     return hipStreamIsCapturing(s, &cs) == hipSuccess && cs != hipStreamCaptureStatusNone;
 }
 
-// After a launch through this reassembler on stream s (caller holds r->mu): remember where
-// the stream is, so a later snapshot can wait for exactly these launches.
+// After a launch through this reassembler on stream s (caller holds r->mu): remember the
+// stream, so a later snapshot waits for exactly the streams this reassembler used.
 static hipError_t note_launch(e2sar_hip_reas *r, hipStream_t s)
 {
-    if (capturing(s)) {
-        r->sawCapture = true;          // replays run wherever the caller puts them
-        return hipSuccess;
-    }
-    hipEvent_t &ev = r->done[s];
-    if (!ev) {
-        hipError_t e = hipEventCreateWithFlags(&ev, hipEventDisableTiming);
-        if (e != hipSuccess) {
-            r->done.erase(s);
-            return e;
-        }
-    }
-    return hipEventRecord(ev, s);
+    if (capturing(s)) r->sawCapture = true;          // replays run wherever the caller puts them
+    else r->streams.insert(s);
+    return hipSuccess;
 }
 
 // reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
@@ -150,8 +143,9 @@ static void free_internal(e2sar_hip_reas *r)
     r->scratch.clear();
     for (void *p : r->retired) (void)hipFree(p);
     r->retired.clear();
-    for (auto &kv : r->done) (void)hipEventDestroy(kv.second);
-    r->done.clear();
+    if (r->waitEv) (void)hipEventDestroy(r->waitEv);
+    r->waitEv = nullptr;
+    r->streams.clear();
 }
 
 // Free whatever a partly built reassembler holds (every pointer starts null).
@@ -809,11 +803,12 @@ int e2sar_hip_reas_gc(e2sar_hip_reas *r, uint64_t now_ms, uint64_t timeout_ms, v
 }
 
 // Wait until every kernel launched through this reassembler has finished (caller holds
-// r->mu, so no new one starts): the events recorded after each launch, one per stream used,
-// not the whole device -- other reassemblers, copy streams and unrelated work run on, and a
-// capture in progress on another thread is not disturbed.  Once a launch of this reassembler
-// has been captured into a graph, its replays can run on any stream, so the wait falls back
-// to the device.
+// r->mu, so no new one starts): an event recorded now on each stream it launched on, not
+// the whole device -- other reassemblers, copy streams and unrelated work run on, and a
+// capture in progress on another thread is not disturbed.  A stream the caller destroyed
+// since (its handle no longer valid) finished its work when it was destroyed.  Once a
+// launch of this reassembler has been captured into a graph, its replays can run on any
+// stream, so the wait falls back to the device.
 static int wait_launches(e2sar_hip_reas *r)
 {
     HIP_TRY(hipSetDevice(r->ctx->device));
@@ -821,7 +816,18 @@ static int wait_launches(e2sar_hip_reas *r)
         HIP_TRY(hipDeviceSynchronize());
         return E2SAR_HIP_OK;
     }
-    for (auto &kv : r->done) HIP_TRY(hipEventSynchronize(kv.second));
+    if (!r->waitEv) HIP_TRY(hipEventCreateWithFlags(&r->waitEv, hipEventDisableTiming));
+    for (auto it = r->streams.begin(); it != r->streams.end();) {
+        const hipError_t e = hipEventRecord(r->waitEv, *it);
+        if (e == hipErrorInvalidHandle || e == hipErrorContextIsDestroyed || e == hipErrorInvalidResourceHandle) {
+            (void)hipGetLastError();
+            it = r->streams.erase(it);                 // destroyed stream: nothing left to wait for
+            continue;
+        }
+        if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
+        HIP_TRY(hipEventSynchronize(r->waitEv));
+        ++it;
+    }
     return E2SAR_HIP_OK;
 }
 
@@ -1027,6 +1033,28 @@ int e2sar_hip_route_foreign(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32
 {
     return route(ctx, d_packets, stride, d_lens, nPackets, withLBHeader, world, self, 1, d_sendPackets, d_sendLens,
                  d_counts, d_workspace, workspaceBytes, stream);
+}
+
+int e2sar_hip_route_append(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride, const uint32_t *d_lens,
+                           uint32_t nPackets, int withLBHeader, uint32_t world, uint32_t self, int foreignOnly,
+                           uint8_t *d_sendPackets, uint32_t *d_sendLens, uint32_t capPerRank, uint32_t *d_running,
+                           void *d_workspace, size_t workspaceBytes, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (world == 0 || world > 64 || self >= world) return fail(E2SAR_HIP_ERR_PARAMETER, "world must be 1..64, self < world");
+    if ((stride & 15u) || stride < 48u) return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16, >= 48");
+    if (capPerRank == 0 || (uint64_t)capPerRank * world > 0xFFFFFFFFull)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "capPerRank must be > 0 and capPerRank * world < 2^32");
+    if (!d_running) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL running counters");
+    if (nPackets && (!d_packets || !d_lens || !d_sendPackets || !d_sendLens || !d_workspace))
+        return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (workspaceBytes < route_workspace_bytes(nPackets, world)) return fail(E2SAR_HIP_ERR_PARAMETER, "workspace too small");
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    hipError_t e = launch_route(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, foreignOnly ? 1 : 0,
+                                d_sendPackets, d_sendLens, nullptr, d_workspace, s, capPerRank, d_running);
+    if (e != hipSuccess) return hip_fail(e, "route launch");
+    return E2SAR_HIP_OK;
 }
 
 int e2sar_hip_reas_set_owner(e2sar_hip_reas *r, uint32_t world, uint32_t self)

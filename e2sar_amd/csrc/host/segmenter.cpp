@@ -155,25 +155,22 @@ static void init_impl(Segmenter::Impl &m)
 {
     m.useV6 = m.flags.dpV6 && m.uri.has_dataAddrv6();
     if (!m.uri.has_dataAddrv4() && m.uri.has_dataAddrv6()) m.useV6 = true;
-    // outgoing interface and its MTU for the URI's data address (e2sarDPSegmenter.cpp:56-110):
-    // mtu 0 takes the interface's MTU, an override must not exceed it (an interface that
-    // reports 0 accepts any override).  The device slot layout is sized for the
-    // reference's 9000-byte limit, so an auto-detected MTU above it (loopback reports
-    // 65536) is capped at 9000.
+    // outgoing interface and its MTU for the URI's data address (e2sarDPSegmenter.cpp:56-110),
+    // with the reference's rules: a failed lookup throws whatever the override; mtu 0 takes
+    // the interface's MTU as reported (loopback's 65536 then fails the 9000-byte sanity
+    // check below, as in the reference, hpp:307-308); an override must not exceed the
+    // interface's MTU (an interface that reports 0 accepts any override).
     auto addr = m.useV6 ? m.uri.get_dataAddrv6() : m.uri.get_dataAddrv4();
     if (addr.has_error()) throw E2SARException("Data address is not present in the URI");
     auto intf = NetUtil::getInterfaceAndMTU(addr.value().first);
-    uint16_t ifMtu = 0;
-    if (intf.has_value()) {
-        m.iface = std::get<0>(intf.value());
-        ifMtu = std::get<1>(intf.value());
-    } else if (m.flags.mtu == 0) {
+    if (!intf.has_value())
         throw E2SARException("Unable to determine outgoing interface for LB destination address " +
                              addr.value().first + ": " + intf.error().message());
-    }
+    m.iface = std::get<0>(intf.value());
+    const uint32_t ifMtu = std::get<1>(intf.value());
     if (m.flags.mtu == 0) {
         if (ifMtu == 0) throw E2SARException("Outgoing interface MTU is reported as 0, please use manual override of MTU size");
-        m.mtu = std::min<uint16_t>(ifMtu, 9000);
+        m.mtu = ifMtu;
     } else {
         if (ifMtu > 0 && m.flags.mtu > ifMtu)
             throw E2SARException("Segmenter flags MTU override value exceeds outgoing interface MTU of " + m.iface);

@@ -327,7 +327,10 @@ result<std::tuple<std::string, uint16_t>> getInterfaceAndMTU(const std::string &
     const int rc = ioctl(fd, SIOCGIFMTU, &ifr);
     close(fd);
     if (rc != 0) return E2SARErrorInfo{E2SARErrorc::SocketError, std::string("SIOCGIFMTU: ") + strerror(errno)};
-    return std::make_tuple(name, (uint16_t)std::min(ifr.ifr_mtu, 65535));
+    // the MTU travels as u_int16_t, as in the reference (e2sarNetUtil.cpp:147-149 narrows
+    // getMTU's size_t): loopback's 65536 reads as 0 there ("lo doesn't" report one,
+    // e2sarDPSegmenter.cpp:86-88), and so it does here
+    return std::make_tuple(name, (uint16_t)ifr.ifr_mtu);
 }
 
 }  // namespace NetUtil

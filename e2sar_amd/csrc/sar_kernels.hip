@@ -2122,9 +2122,14 @@ __global__ __launch_bounds__(kBlock) void route_hist_kernel(const uint8_t *__res
 // For each destination the nBlocks counts are scanned 256 at a time (wave prefix sums
 // through LDS, a running carry between tiles), so the scan costs nBlocks/256 block steps
 // per destination instead of nBlocks dependent loads.
+// Append mode (cap > 0): rank d's span is a region of cap slots at d * cap that successive
+// batches append to; destBase[d] = d * cap + running[d], then running[d] += this batch's
+// count (the count keeps growing past cap, so the caller sees an overflow; the pack kernel
+// writes nothing past a region's end).  counts may be NULL in append mode.
 __global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict__ blockHist, uint32_t nBlocks,
                                                             uint32_t world, uint32_t *__restrict__ counts,
-                                                            uint32_t *__restrict__ destBase)
+                                                            uint32_t *__restrict__ destBase, uint32_t cap,
+                                                            uint32_t *__restrict__ running)
 {
     __shared__ uint32_t waveSum[kBlock / 64];
     __shared__ uint32_t tot[kMaxWorld];
@@ -2152,15 +2157,21 @@ __global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict
         }
         if (threadIdx.x == 0) {
             tot[d] = carry;
-            counts[d] = carry;
+            if (counts) counts[d] = carry;
         }
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         uint32_t run = 0;
         for (uint32_t d = 0; d < world; d++) {
-            destBase[d] = run;
-            run += tot[d];
+            if (cap) {
+                const uint32_t have = running[d];
+                destBase[d] = d * cap + have;
+                running[d] = have + tot[d];
+            } else {
+                destBase[d] = run;
+                run += tot[d];
+            }
         }
     }
 }
@@ -2182,7 +2193,7 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
                                                             const uint32_t *__restrict__ lens, uint32_t n, int withLB,
                                                             uint32_t world, uint32_t self, int excludeSelf,
                                                             const uint32_t *__restrict__ blockBase,
-                                                            const uint32_t *__restrict__ destBase,
+                                                            const uint32_t *__restrict__ destBase, uint32_t cap,
                                                             uint8_t *__restrict__ out, uint32_t *__restrict__ outLens)
 {
     __shared__ uint32_t pos[kBlock];
@@ -2203,8 +2214,10 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
         uint32_t before = 0;
         for (uint32_t w = 0; w < wv; w++) before += waveCnt[w][dest];
         const uint32_t q = destBase[dest] + blockBase[(uint64_t)g * world + dest] + before + rank;
-        pos[threadIdx.x] = q;
-        if (sl == 0) outLens[q] = lens[p];
+        if (!cap || q < (dest + 1u) * cap) {                  // append mode: nothing past the region
+            pos[threadIdx.x] = q;
+            if (sl == 0) outLens[q] = lens[p];
+        }
     }
     // foreign-only routing leaves most blocks with nothing to move at small world sizes
     if (!__syncthreads_or(dest != kNoDest)) return;
@@ -2253,18 +2266,20 @@ size_t route_workspace_bytes(uint32_t n, uint32_t world)
 
 hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
                         uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
-                        uint32_t *counts, void *workspace, hipStream_t stream)
+                        uint32_t *counts, void *workspace, hipStream_t stream, uint32_t cap, uint32_t *running)
 {
     if (world == 0 || world > kMaxWorld || self >= world) return hipErrorInvalidValue;
-    if (n == 0) return launch_zero_words(counts, world, stream);
+    if (cap && (uint64_t)cap * world > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if (n == 0) return counts ? launch_zero_words(counts, world, stream) : hipSuccess;
     const uint32_t nb = cdiv(n, kBlock);
     uint32_t *blockHist = static_cast<uint32_t *>(workspace);
     uint32_t *destBase = blockHist + (size_t)nb * world;
     hipLaunchKernelGGL(route_hist_kernel, dim3(nb), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
                        self, excludeSelf, blockHist);
-    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kBlock), 0, stream, blockHist, nb, world, counts, destBase);
+    hipLaunchKernelGGL(route_scan_kernel, dim3(1), dim3(kBlock), 0, stream, blockHist, nb, world, counts, destBase,
+                       cap, running);
     hipLaunchKernelGGL(route_pack_kernel, dim3(nb * kPackSplit), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB, world,
-                       self, excludeSelf, blockHist, destBase, out, outLens);
+                       self, excludeSelf, blockHist, destBase, cap, out, outLens);
     return hipGetLastError();
 }
 

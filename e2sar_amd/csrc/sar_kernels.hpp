@@ -209,6 +209,7 @@ hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t st
 size_t route_workspace_bytes(uint32_t n, uint32_t world);
 hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
                         uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
-                        uint32_t *counts, void *workspace, hipStream_t stream);
+                        uint32_t *counts, void *workspace, hipStream_t stream, uint32_t cap = 0,
+                        uint32_t *running = nullptr);   // cap > 0: append to per-rank regions of cap slots
 
 }  // namespace e2sar_amd

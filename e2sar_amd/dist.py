@@ -112,6 +112,88 @@ def exchange(send_pk: torch.Tensor, send_ln: torch.Tensor, counts: Union[Sequenc
     return recv_pk, recv_ln, n_recv
 
 
+def exchange_regions(send_pk: torch.Tensor, send_ln: torch.Tensor, running: torch.Tensor, cap: int, stride: int,
+                     group: Optional[dist.ProcessGroup] = None,
+                     out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
+    """All-to-all-v of per-rank regions filled by ``RegionRouter``: rank d's datagrams are
+    the first running[d] slots of region d (slots [d*cap, d*cap + running[d]) of send_pk /
+    send_ln).  Split sizes from one all-gather of the running counters (one host read).
+    nccl: one all_to_all over the region views (RCCL send/recv per peer, no packing copy);
+    gloo: the regions are gathered on the host and sent with all_to_all_single.  Returns
+    (recv_pk, recv_ln, n_recv), received spans contiguous in source-rank order."""
+    world = dist.get_world_size(group)
+    rank = dist.get_rank(group)
+    m = count_matrix(running, group)
+    if any(c > cap for row in m for c in row):
+        raise RuntimeError(f"route regions overflowed (cap {cap} datagrams per rank): {m}")
+    sc, rc = m[rank], [m[s][rank] for s in range(world)]
+    n_recv = sum(rc)
+    dev = send_pk.device
+    if out is not None and out[0].numel() >= n_recv * stride and out[1].numel() >= n_recv and out[0].device == dev:
+        recv_pk, recv_ln = out
+    else:
+        recv_pk = torch.empty(max(n_recv, 1) * stride, dtype=torch.uint8, device=dev)
+        recv_ln = torch.empty(max(n_recv, 1), dtype=torch.int32, device=dev)
+    if not any(any(row) for row in m):
+        return recv_pk, recv_ln, 0                          # no rank sends anything: skip the collective
+    roff = [sum(rc[:s]) for s in range(world)]
+    if _via_host(group, send_pk):
+        spk = torch.cat([send_pk[d * cap * stride:(d * cap + sc[d]) * stride].cpu() for d in range(world)])
+        sln = torch.cat([send_ln[d * cap:d * cap + sc[d]].cpu() for d in range(world)])
+        hpk, hln = torch.empty(n_recv * stride, dtype=torch.uint8), torch.empty(n_recv, dtype=torch.int32)
+        dist.all_to_all_single(hpk, spk, [c * stride for c in rc], [c * stride for c in sc], group=group)
+        dist.all_to_all_single(hln, sln, rc, sc, group=group)
+        recv_pk[: n_recv * stride].copy_(hpk)
+        recv_ln[:n_recv].copy_(hln)
+    else:
+        dist.all_to_all([recv_pk[roff[s] * stride:(roff[s] + rc[s]) * stride] for s in range(world)],
+                        [send_pk[d * cap * stride:(d * cap + sc[d]) * stride] for d in range(world)], group=group)
+        dist.all_to_all([recv_ln[roff[s]:roff[s] + rc[s]] for s in range(world)],
+                        [send_ln[d * cap:d * cap + sc[d]] for d in range(world)], group=group)
+    return recv_pk, recv_ln, n_recv
+
+
+class RegionRouter:
+    """Routes a stream of landed batches, one launch per batch, into per-rank regions of
+    cap datagram slots (e2sar_hip_route_append); ``exchange_regions`` sends them once per
+    step.  Routing a batch right after it landed reads it from the Infinity Cache."""
+
+    def __init__(self, ctx, stride: int, cap: int, max_batch: int, world: int, rank: int,
+                 with_lb_header: bool = True, foreign_only: bool = True):
+        from ._capi import lib
+        self.ctx = ctx
+        self.stride, self.cap, self.world, self.rank = stride, cap, world, rank
+        self.with_lb, self.foreign_only, self.max_batch = with_lb_header, foreign_only, max_batch
+        d = ctx.torch_device
+        self.send_pk = torch.empty(world * cap * stride, dtype=torch.uint8, device=d)
+        self.send_ln = torch.empty(world * cap, dtype=torch.int32, device=d)
+        self.running = torch.zeros(world, dtype=torch.int32, device=d)
+        ws = int(lib().e2sar_hip_route_workspace_bytes(max_batch, world))
+        self.workspace = torch.empty(max(ws, 16), dtype=torch.uint8, device=d)
+
+    def reset(self) -> None:
+        """Empty the regions (a fill kernel on the context stream: capture-safe)."""
+        from ._capi import check, lib
+        check(lib().e2sar_hip_memset_d(self.ctx.handle, C.c_void_p(self.running.data_ptr()), 0,
+                                        self.running.numel() * 4))
+
+    def route(self, pk: torch.Tensor, ln: torch.Tensor, n: int, stream: Optional[torch.cuda.Stream] = None):
+        from ._capi import check, lib
+        from .sar import _stream_handle
+        if n > self.max_batch:
+            raise ValueError("batch larger than the router was sized for")
+        check(lib().e2sar_hip_route_append(
+            self.ctx.handle, C.c_void_p(pk.data_ptr()), self.stride, C.c_void_p(ln.data_ptr()), n,
+            1 if self.with_lb else 0, self.world, self.rank, 1 if self.foreign_only else 0,
+            C.c_void_p(self.send_pk.data_ptr()), C.c_void_p(self.send_ln.data_ptr()), self.cap,
+            C.c_void_p(self.running.data_ptr()), C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(),
+            C.c_void_p(_stream_handle(stream))))
+
+    def exchange(self, group: Optional[dist.ProcessGroup] = None,
+                 out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None):
+        return exchange_regions(self.send_pk, self.send_ln, self.running, self.cap, self.stride, group, out)
+
+
 class PacketRouter:
     """Packs a landed datagram batch into per-owner spans on the GPU."""
 

@@ -396,6 +396,22 @@ int e2sar_hip_route_foreign(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32
                             uint32_t *d_sendLens, uint32_t *d_counts, void *d_workspace,
                             size_t workspaceBytes, void *stream);
 
+/* Per-batch routing into per-rank regions, for a stream of landed batches exchanged once
+ * per step: rank d's datagrams go to slots [d*capPerRank + running[d], ...) of
+ * d_sendPackets / d_sendLens (stable order, appended after the earlier batches'), and
+ * running[d] (device, world counters, zeroed by the caller before the first batch, e.g.
+ * e2sar_hip_memset_d) grows by this batch's count for d.  A datagram that would land past
+ * its region is not written, but still counted: running[d] > capPerRank after the step
+ * means the regions were too small.  foreignOnly: as e2sar_hip_route_foreign (this rank's
+ * datagrams and unparsable ones stay here, running[self] stays 0).  Routing each batch
+ * right after it landed reads it while it is still in the Infinity Cache; the step's one
+ * all-to-all then sends each region's first running[d] slots.  Asynchronous. */
+int e2sar_hip_route_append(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_t stride,
+                           const uint32_t *d_lens, uint32_t nPackets, int withLBHeader,
+                           uint32_t world, uint32_t self, int foreignOnly, uint8_t *d_sendPackets,
+                           uint32_t *d_sendLens, uint32_t capPerRank, uint32_t *d_running,
+                           void *d_workspace, size_t workspaceBytes, void *stream);
+
 /* Ownership of a reassembler in a world of `world` ranks (1..64): from the next launch on,
  * a datagram whose RE header parses but whose eventNum % world != self belongs to another
  * rank and takes no part -- not counted in any statistic, no byte copied.  Unparsable

@@ -164,6 +164,7 @@ struct e2o_reas {
     lost *lqHead, *lqTail;            /* lostEventsQueue */
     uint64_t now;
     e2o_reas_stats st;
+    uint64_t lastPopFrags;            /* numFragments of the event last handed out (test access) */
 };
 
 /* pair_hash (e2sarUtil.hpp:526-533) */
@@ -317,9 +318,14 @@ int e2o_reas_pop(e2o_reas *r, uint8_t **event, size_t *bytes, uint64_t *eventNum
     *bytes = it->bytes;
     *eventNum = it->eventNum;
     *dataId = it->dataId;
+    r->lastPopFrags = it->numFragments;
     free(it);
     return 0;
 }
+
+/* numFragments (cpp:398) of the event the last pop handed out: the reference keeps it in
+ * the EventQueueItem; getEvent does not return it, the tests compare the device's count */
+uint64_t e2o_reas_last_pop_frags(const e2o_reas *r) { return r->lastPopFrags; }
 
 void e2o_reas_push_batch(e2o_reas *r, const uint8_t *pkts, size_t n, size_t stride,
                          const uint32_t *lens)

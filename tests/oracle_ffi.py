@@ -54,6 +54,8 @@ def lib() -> C.CDLL:
         L.e2o_reas_set_time.argtypes = [vp, C.c_uint64]
         L.e2o_reas_push.restype = None
         L.e2o_reas_push.argtypes = [vp, u8p, sz]
+        L.e2o_reas_last_pop_frags.restype = C.c_uint64
+        L.e2o_reas_last_pop_frags.argtypes = [vp]
         L.e2o_reas_push_batch.restype = None
         L.e2o_reas_push_batch.argtypes = [vp, u8p, sz, sz, u8p]
         L.e2o_reas_pop.restype = C.c_int
@@ -140,6 +142,15 @@ class Reassembler:
         if n == -2:
             raise ValueError("event larger than pop buffer")
         return buf[:n].tobytes(), ev.value, d.value
+
+    def pop_all_frags(self, cap: int = 1 << 26):
+        """(bytes, eventNum, dataId, numFragments) of every queued event."""
+        out = []
+        while True:
+            r = self.pop(cap)
+            if r is None:
+                return out
+            out.append(r + (int(lib().e2o_reas_last_pop_frags(self.h)),))
 
     def pop_all(self, cap: int = 1 << 26):
         out = []

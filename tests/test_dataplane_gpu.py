@@ -596,11 +596,11 @@ def test_late_offset0_through_the_facade(E, reference_order):
 
 def test_mtu_auto_detect_from_the_outgoing_interface(E):
     # mtu 0: the MTU of the interface the data address routes through
-    # (e2sarDPSegmenter.cpp:56-110); loopback reports 65536, capped at the 9000-byte limit
-    # the device slot layout shares with the reference's override check (hpp:310-311)
+    # (e2sarDPSegmenter.cpp:56-110).  The reference carries it as u_int16_t
+    # (e2sarNetUtil.cpp:147-149), so loopback's 65536 reads as 0 and mtu 0 is refused with
+    # the reference's message; an override is accepted as is ("lo doesn't" report an MTU)
     port = next_port()
-    seg = make_seg(E, port, mtu=0)
-    assert seg.getIntf() == "lo"
-    assert seg.getMTU() == 9000 and seg.getMaxPldLen() == 9000 - 64
+    with pytest.raises(Exception, match="reported as 0"):
+        make_seg(E, port, mtu=0)
     seg2 = make_seg(E, port, mtu=1500)
     assert seg2.getIntf() == "lo" and seg2.getMTU() == 1500

@@ -6,10 +6,13 @@ oracle's reassembly of the datagrams that rank processed:
 
 * ``all``: route every landed datagram to its owner (e2sar_hip_route_batch, self
   included), one all-to-all-v, reassemble what arrived;
-* ``foreign`` (what bench.py's spread leg runs): reassemble the datagrams this rank owns
-  where they landed (e2sar_hip_reas_set_owner), route only the foreign ones
-  (e2sar_hip_route_foreign), exchange them (split sizes from one all-gather of the device
-  count vectors), reassemble what arrived.
+* ``foreign``: reassemble the datagrams this rank owns where they landed
+  (e2sar_hip_reas_set_owner), route only the foreign ones (e2sar_hip_route_foreign),
+  exchange them (split sizes from one all-gather of the device count vectors), reassemble
+  what arrived;
+* ``regions`` (what bench.py's spread leg runs): as ``foreign``, but the landed stream
+  comes in batches, each routed into per-rank regions right after it landed
+  (e2sar_hip_route_append), and one exchange of the regions follows the last batch.
 
 Two ranks share GPU 0 over gloo (all-to-all staged through host memory; RCCL refuses two
 ranks on one device).  The RCCL branch itself runs at world 1 in a fresh child process
@@ -35,7 +38,7 @@ def _spread_rank(rank, world, mode, corrupt=True):
     import oracle_ffi as O
     import sar_inputs as S
     from e2sar_amd import sar
-    from e2sar_amd.dist import PacketRouter, exchange
+    from e2sar_amd.dist import PacketRouter, RegionRouter, exchange
 
     ctx = sar.Context(0)
     mtu = 1500
@@ -70,12 +73,24 @@ def _spread_rank(rank, world, mode, corrupt=True):
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, arena_bytes=1 << 22)
     hp_l = lpk[: nl * stride].view(nl, stride).cpu().numpy()
     hl_l = lln[:nl].cpu().numpy().astype(np.uint32)
-    if mode == "foreign":
+    if mode in ("foreign", "regions"):
         R.set_owner(world, rank)
-        R.reassemble(lpk, stride, lln, nl)                    # this rank's events, in place
-        spk, sln, cnt = router.route(lpk, lln, nl, foreign_only=True)
-        rpk, rln, nr = exchange(spk, sln, cnt, stride)       # device counts: one host read
-        counts = [int(c) for c in cnt.tolist()]
+        if mode == "foreign":
+            R.reassemble(lpk, stride, lln, nl)                # this rank's events, in place
+            spk, sln, cnt = router.route(lpk, lln, nl, foreign_only=True)
+            rpk, rln, nr = exchange(spk, sln, cnt, stride)   # device counts: one host read
+            counts = [int(c) for c in cnt.tolist()]
+        else:
+            # bench.py's spread leg: the landed stream in batches (a cut inside events), each
+            # reassembled in place and appended to per-rank regions, one exchange at the end
+            rr = RegionRouter(ctx, stride, nl, nl, world, rank)
+            rr.reset()
+            cut = nl // 3 + 1
+            for a, b in ((0, cut), (cut, nl)):
+                R.reassemble(lpk[a * stride:], stride, lln[a:], b - a)
+                rr.route(lpk[a * stride:], lln[a:], b - a)
+            rpk, rln, nr = rr.exchange()
+            counts = [int(c) for c in rr.running.tolist()]
         R.set_cold(True)
         R.reassemble(rpk, stride, rln, nr)
         # what this rank processed: the landed datagrams it keeps + what it received
@@ -159,8 +174,25 @@ def _nccl_worker(port, result_q):
         rpk, rln, nr = exchange(spk, sln, [n], stride)
         out["raw"] = bool(nr == n and torch.equal(rpk[: n * stride], spk) and torch.equal(rln[:n], sln)
                           and rpk.is_cuda)
-        for mode in ("all", "foreign"):
+        for mode in ("all", "foreign", "regions"):
             out[mode] = _spread_rank(0, 1, mode, corrupt=False)
+        # the regions path's RCCL branch (all_to_all over region views) with data in flight:
+        # every datagram routed to rank 0 itself (route_append without foreign_only)
+        from e2sar_amd.dist import RegionRouter
+        from e2sar_amd import sar
+        ctx = sar.Context(0)
+        rr = RegionRouter(ctx, stride, 2 * n, n, 1, 0, with_lb_header=True, foreign_only=False)
+        rr.reset()
+        spk2 = spk.clone()
+        for k in range(n):                                 # parsable RE headers: version 1, eventNum k
+            spk2[k * stride + 16] = 0x10
+            spk2[k * stride + 17] = 0
+        sln2 = torch.full((n,), stride, dtype=torch.int32, device="cuda")
+        rr.route(spk2, sln2, n // 2)
+        rr.route(spk2[(n // 2) * stride:], sln2[n // 2:], n - n // 2)
+        rpk2, rln2, nr2 = rr.exchange()
+        out["regions_raw"] = bool(nr2 == n and torch.equal(rpk2[: n * stride], spk2[: n * stride])
+                                  and torch.equal(rln2[:n], sln2))
         out["backend"] = dist.get_backend()
     finally:
         dist.destroy_process_group()
@@ -197,7 +229,7 @@ def _run(target, args, nproc, timeout=150):
     return res
 
 
-@pytest.mark.parametrize("mode", ["all", "foreign"])
+@pytest.mark.parametrize("mode", ["all", "foreign", "regions"])
 def test_spread_landing_route_exchange_reassemble_two_ranks(mode):
     port = _free_port()
     world = 2
@@ -208,7 +240,7 @@ def test_spread_landing_route_exchange_reassemble_two_ranks(mode):
     # 0) misses that fragment
     assert res[1][5]["badHeaderDiscards"][0] == 1 and res[0][5]["badHeaderDiscards"][0] == 0
     assert res[0][5]["inProgress"] == (1, 1) and res[1][5]["inProgress"] == (0, 0)
-    if mode == "foreign":
+    if mode != "all":
         # nothing a rank owns is packed for itself
         assert res[0][3][0] == 0 and res[1][3][1] == 0
 
@@ -218,10 +250,12 @@ def test_rccl_exchange_world1_fresh_process():
     (out,) = _run(_nccl_worker, [(_free_port(),)], 1, timeout=240)
     assert out["backend"] == "nccl"
     assert out["raw"], "RCCL all-to-all of datagram slots changed bytes"
-    for mode in ("all", "foreign"):
+    assert out["regions_raw"], "RCCL all_to_all of region views changed bytes"
+    for mode in ("all", "foreign", "regions"):
         rank, ok, mine, counts, nr, stat_ok = out[mode]
         assert ok, (mode, mine, counts, nr, stat_ok)
         assert mine == [100 + i for i in range(13)]
     # route_batch sends every datagram to rank 0 through RCCL; foreign-only routing keeps them
     assert out["all"][3] == [out["all"][4]] and out["all"][4] > 0
     assert out["foreign"][3] == [0] and out["foreign"][4] == 0
+    assert out["regions"][3] == [0] and out["regions"][4] == 0

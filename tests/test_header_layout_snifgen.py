@@ -95,3 +95,44 @@ def test_header_classes_match_snifgen():
     re = e2sar_py.REHdr()
     re.set(0x10E1, 1436, 1 << 20, 0x0102030405060708)
     assert struct.unpack(RE_FMT, re.to_bytes()) == (0x10, 0, 0x10E1, 1436, 1 << 20, 0x0102030405060708)
+
+
+# LBHdrV3 as e2sarHeaders.hpp:191-198 declares it (packed, network byte order): preamble
+# char[2] 'LB', version u8 (lbhdrVersion3 = 3), nextProto u8 (rehdrVersion = 1),
+# slotSelect u16, portSelect u16, tick u64 -- and _send fills it with
+# lb3.set(lbEventNum & 0xFFFF, entropy, lbEventNum) (e2sarDPSegmenter.cpp:753).  This is a
+# restatement of the reference's own struct, not a second independent definition (snifgen
+# has none for v3), so it pins the member order the header declares; DESIGN.md 5.1 records
+# that no reference-held vector covers v3 bytes.
+LB3_FMT = "!2sBBHHQ"        # e2sarHeaders.hpp:193-198
+assert struct.calcsize(LB3_FMT) == 16
+
+
+def decode_v3(hdr: bytes):
+    pre, ver, proto, slot, port, tick = struct.unpack(LB3_FMT, hdr[:16])
+    return dict(pre=pre, ver=ver, proto=proto, slot=slot, port=port, tick=tick)
+
+
+def test_v3_headers_decode_with_the_reference_struct_order():
+    mp = O.max_pld_len(1500)
+    stride = (36 + mp + 15) // 16 * 16
+    ev = np.random.default_rng(3).integers(0, 256, 5000, dtype=np.uint8)
+    entropy, tick = 0xBEEF, 0x0123456789ABCDEF
+    pk, ln = O.segment_event(ev, 7, 0x10E1, entropy, tick, 3, mp, stride)
+    for k in range(len(ln)):
+        h = decode_v3(pk[k, :16].tobytes())
+        assert (h["pre"], h["ver"], h["proto"]) == (b"LB", 3, 1)
+        assert h["slot"] == tick & 0xFFFF and h["port"] == entropy and h["tick"] == tick
+    with open(os.path.join(HERE, "golden", "sar_golden.json")) as f:
+        golden = json.load(f)
+    n = 0
+    for case in golden["segment"]:
+        if case["lbHdrVersion"] != 3:
+            continue
+        for e in case["events"]:
+            for key in ("first_hdr", "second_hdr", "last_hdr"):
+                h = decode_v3(bytes.fromhex(e[key]))
+                assert (h["pre"], h["ver"], h["proto"]) == (b"LB", 3, 1)
+                assert h["slot"] == e["lbTick"] & 0xFFFF and h["port"] == e["entropy"] and h["tick"] == e["lbTick"]
+                n += 1
+    assert n > 0

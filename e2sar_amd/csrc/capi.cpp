@@ -70,6 +70,8 @@ struct e2sar_hip_reas {
         size_t roWorkBytes = 0;
         void *tiles = nullptr;
         size_t tilesBytes = 0;
+        void *keys = nullptr;            // group-key pre-pass records of the fused kernel
+        size_t keysBytes = 0;
     };
     std::map<hipStream_t, Scratch> scratch;
     std::vector<void *> retired;
@@ -102,6 +104,12 @@ static hipError_t note_launch(e2sar_hip_reas *r, hipStream_t s)
 // reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
 // that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
 static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
+
+// Group-key pre-pass in front of the fused kernel (reas_keys_kernel; build knob, A/B in
+// DESIGN.md 4.5)
+#ifndef E2SAR_REAS_PREPASS
+#define E2SAR_REAS_PREPASS 1
+#endif
 
 // Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
 // cold (E2SAR_HIP_REAS_COLD_DATAGRAMS), and for a batch too large to still be cached.
@@ -139,6 +147,7 @@ static void free_internal(e2sar_hip_reas *r)
         if (kv.second.roScratch) (void)hipFree(kv.second.roScratch);
         if (kv.second.roWork) (void)hipFree(kv.second.roWork);
         if (kv.second.tiles) (void)hipFree(kv.second.tiles);
+        if (kv.second.keys) (void)hipFree(kv.second.keys);
     }
     r->scratch.clear();
     for (void *p : r->retired) (void)hipFree(p);
@@ -602,7 +611,13 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;
     }
-    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
+    GroupKeys *keys = nullptr;
+    if (E2SAR_REAS_PREPASS) {
+        const size_t kb = sizeof(GroupKeys) * (size_t)reas_launch_groups(r->dev, nPackets, stride);
+        if (int rc = grow(r, s, sc.keys, sc.keysBytes, kb)) return rc;
+        keys = static_cast<GroupKeys *>(sc.keys);
+    }
+    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s, keys);
     if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;

@@ -740,7 +740,7 @@ struct Classified {
 // table and only the run tail adds to the event's byte/fragment counter, so the
 // per-event atomics are per run, not per datagram.
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
-                                    uint64_t now, uint32_t shard)
+                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{})
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
@@ -781,7 +781,22 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     const bool head = ok && (lane == 0 || !pok || pev != ev || pd != d);
     const bool tail = ok && (lane == 63 || !nok || nev != ev || nd != d);
 
-    const LookupResult lr = find_or_create(R, head, ev, d, blen, now);
+    // keys resolved by the group-key pre-pass (reas_keys_kernel): a run head whose key is
+    // one of them takes its slot and buffer from the record instead of the table
+    bool pre = false;
+    LookupResult lr{kNoSlot, 0, kNoBuf};
+    if (hasKeys) {
+#pragma unroll
+        for (int k = 0; k < 2; k++)
+            if (!pre && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
+                pre = true;
+                lr = LookupResult{K.slot[k], K.bytes[k], K.boff[k]};
+            }
+    }
+    {
+        const LookupResult lk = find_or_create(R, head && !pre, ev, d, blen, now);
+        if (!pre) lr = lk;
+    }
 
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
@@ -996,7 +1011,7 @@ struct ReasGroupLds {
 template <int U, bool HO = false>
 __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
-                                           uint32_t g, ReasGroupLds &L)
+                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr)
 {
     const uint32_t tx = threadIdx.x;
     const uint32_t g0 = g * G;
@@ -1004,6 +1019,10 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     const bool w0 = tx < 64;
     const uint32_t lane = tx & 63u;
 
+    // the group's pre-resolved keys (scalar loads, issued first: they ride beside the
+    // header loads instead of a dependent table round trip after them)
+    GroupKeys K{};
+    if (keys) K = keys[g];
     TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
@@ -1061,7 +1080,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 
     unsigned long long old = 0;
     if (w0) {
-        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g);
+        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g, keys != nullptr, K);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -1132,10 +1151,57 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 template <int U>
 __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                            uint32_t stride, const uint32_t *__restrict__ lens,
-                                                                           uint32_t n, uint64_t now, uint32_t G)
+                                                                           uint32_t n, uint64_t now, uint32_t G,
+                                                                           const GroupKeys *__restrict__ keys)
 {
     __shared__ ReasGroupLds L;
-    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L);
+    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys);
+}
+
+// Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
+// datagram), 32 groups per wave.  Runs of equal keys across consecutive lanes collapse to
+// one table lookup (the run head), so an event spread over ~15 groups costs one CAS here
+// instead of ~15 CASes on its slot in reas_kernel, where each sits in front of a
+// group's stores.  Creates the slots and event buffers exactly as the
+// run heads of reas_kernel would (find_or_create), so the results are the same.
+__global__ __launch_bounds__(kBlock) void reas_keys_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                           const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
+                                                           uint32_t G, uint32_t nGroups, GroupKeys *__restrict__ keys)
+{
+    const uint32_t lane = threadIdx.x & 63u;
+    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t g = wave * 32u + (lane >> 1), k = lane & 1u;
+    if (wave * 32u >= nGroups) return;                                   // wave-uniform
+    const bool live = g < nGroups;
+    uint32_t p = 0;
+    if (live) {
+        const uint32_t g0 = g * G, gn = (n - g0 < G) ? n - g0 : G;
+        p = k ? g0 + gn - 1u : g0;
+    }
+    const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
+    const RawHdr raw = load_hdr(R, pkts, stride, lens, p);
+    ParsedHdr h = parse_hdr(raw, hl, stride, live);
+    if (h.ok && foreign_event(R, h.ev)) h.ok = false;
+    const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(h.ev >> 32), 0u) << 32) | lane_prev((uint32_t)h.ev, 0u);
+    const uint32_t pd = lane_prev(h.d, 0u), pok = lane_prev(h.ok ? 1u : 0u, 0u);
+    const bool head = h.ok && (lane == 0 || !pok || pev != h.ev || pd != h.d);
+    const LookupResult lr = find_or_create(R, head, h.ev, h.d, h.blen, now);
+    const uint64_t H = __ballot(head);
+    const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
+    const uint64_t hm = H & le;
+    const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
+    const uint32_t slot = __shfl(lr.slot, myhead);
+    const uint32_t bytes = __shfl(lr.bytes, myhead);
+    const uint64_t boff = shfl_u64(lr.bufOff, myhead);
+    if (live) {
+        GroupKeys *o = keys + g;
+        o->ev[k] = h.ev;
+        o->boff[k] = boff;
+        o->slot[k] = slot;
+        o->bytes[k] = bytes;
+        o->d[k] = h.d;
+        o->valid[k] = (h.ok && slot != kNoSlot) ? 1u : 0u;
+    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1194,7 +1260,7 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(C
     const uint32_t g = local - B.nSeg;
     const uint32_t slots = (B.n - g * B.G < B.G) ? B.n - g * B.G : B.G;
     wait_group_ready(R, B.tiles, g, slots * (stride >> 4));
-    reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L);
+    reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L, nullptr);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1241,6 +1307,65 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
     }
 }
 
+// Scatter stores: 1 = destination-aligned (shift_store: source-aligned loads, the next
+// chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 0 = source-aligned
+// chunks stored at their misaligned destination (scatter_chunk), the round-2 form.
+#ifndef E2SAR_SCATTER_SHIFT
+#define E2SAR_SCATTER_SHIFT 1
+#endif
+
+// Bytes [s, s+16) of the 32-byte register pair lo:hi (s in 0..15, lane-varying): a funnel
+// shift, v_alignbyte after a dword select.
+__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, uint32_t s)
+{
+    const uint32_t q = s >> 2, r = s & 3u;
+    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
+    uint32_t t[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++)
+        t[k] = (q == 0u) ? w[k] : (q == 1u) ? w[k + 1] : (q == 2u) ? w[k + 2] : w[k + 3];
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(t[1], t[0], r);
+    o.y = __builtin_amdgcn_alignbyte(t[2], t[1], r);
+    o.z = __builtin_amdgcn_alignbyte(t[3], t[2], r);
+    o.w = __builtin_amdgcn_alignbyte(t[4], t[3], r);
+    return o;
+}
+
+// Destination-aligned store of the chunk pair (own = datagram bytes [16c, 16c+16), next =
+// [16c+16, 16c+32)) of a classified datagram.  Payload byte t sits at slot offset hl + t
+// and goes to dst + t; with a = dst mod 16, the aligned event block b ((dst & ~15) + 16b)
+// takes slot bytes [hl - a + 16b, +16) = chunk pair (b + q, b + q + 1) shifted by
+// sigma, q = (hl - a) / 16, sigma = (hl - a) mod 16.  So the lane holding chunk c writes
+// block c - q: loads stay source-aligned and independent of the work record (issued
+// before it arrives), stores are aligned 16-byte stores except at the payload's two
+// edges.  Every block of the payload is written by exactly one chunk: the last needs
+// c = nb - 1 + q <= spc - 1 because a + plen <= 16 * spc - 16q.
+__device__ __forceinline__ void shift_store(const PktInfo pi, uint32_t c, u32x4 own, u32x4 next)
+{
+    if (pi.plen == 0u) return;
+    const uint32_t a = (uint32_t)pi.dst & 15u;
+    const uint32_t dlt = pi.hl - a;                              // hl (20 / 36) > 15 >= a
+    const uint32_t q = dlt >> 4;
+    if (c < q) return;
+    const uint32_t b = c - q;
+    if (16u * b >= a + pi.plen) return;                           // past the payload
+    const u32x4 o = funnel16(own, next, dlt & 15u);
+    uint8_t *D = reinterpret_cast<uint8_t *>((pi.dst & ~15ull) + 16ull * b);
+    const uint32_t lo = (b == 0u) ? a : 0u;
+    const uint32_t hi = (a + pi.plen - 16u * b < 16u) ? a + pi.plen - 16u * b : 16u;
+    if (lo == 0u && hi == 16u) {
+        st16_nt(D, o);
+        return;
+    }
+#pragma unroll
+    for (uint32_t d = 0; d < 4; d++)
+        if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
+    const uint32_t l4 = (lo + 3u) & ~3u, h4 = hi & ~3u;          // partial dwords at the edges
+    if (lo < l4) store_bytes(D, o, lo, l4 < hi ? l4 : hi);
+    if (h4 < hi && h4 >= l4) store_bytes(D, o, h4, hi);
+}
+
 // One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
 template <int U, bool NT>
 __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
@@ -1259,8 +1384,12 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     const uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
-    u32x4 x[U];
+    const bool last = (threadIdx.x & 63u) == 63u;
+    u32x4 x[U], xn[U];
     uint32_t pp[U], cc[U];
+    // chunk i of the group: the chunk index space is the slots' bytes, so chunk i + 1 is the
+    // next 16 bytes; a wave's lane 63 loads it itself (its neighbour is in another wave),
+    // every other lane takes it from lane + 1
     auto issue = [&](uint32_t r0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -1271,7 +1400,10 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
             else if ((p + 1u) * spc <= ic) p++;
             pp[u] = p;
             cc[u] = ic - p * spc;
-            x[u] = NT ? ld16_nt(bpk + (uint64_t)p * stride + 16u * cc[u]) : ld16(bpk + (uint64_t)p * stride + 16u * cc[u]);
+            const uint8_t *src = bpk + (uint64_t)p * stride + 16u * cc[u];
+            x[u] = NT ? ld16_nt(src) : ld16(src);
+            xn[u] = u32x4{0u, 0u, 0u, 0u};
+            if (E2SAR_SCATTER_SHIFT && last && cc[u] + 1u < spc) xn[u] = NT ? ld16_nt(src + 16) : ld16(src + 16);
         }
     };
     issue(0);
@@ -1293,9 +1425,21 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
         if (r0) issue(r0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
+            // next chunk from lane + 1 (whole wave active: DPP reads every lane)
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+#if E2SAR_SCATTER_SHIFT
+            u32x4 nx;
+            nx.x = lane_next(x[u].x, 0u);
+            nx.y = lane_next(x[u].y, 0u);
+            nx.z = lane_next(x[u].z, 0u);
+            nx.w = lane_next(x[u].w, 0u);
+            if (last) nx = xn[u];
+            if (i >= nch) continue;
+            shift_store(sinfo[pp[u]], cc[u], x[u], nx);
+#else
             if (i >= nch) continue;
             scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
+#endif
         }
     }
 
@@ -1932,13 +2076,25 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG)
     return G;
 }
 
+uint32_t reas_launch_groups(const ReasDev &R, uint32_t n, uint32_t stride)
+{
+    return n ? cdiv(n, reas_group_size(n, stride, R.groupSize)) : 0u;
+}
+
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream, GroupKeys *keys)
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
     const uint32_t G = reas_group_size(n, stride, R.groupSize);
-    hipLaunchKernelGGL((reas_kernel<U>), dim3(cdiv(n, G)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G);
+    const uint32_t groups = cdiv(n, G);
+    if (keys) {
+        const uint32_t waves = cdiv(groups, 32u);
+        hipLaunchKernelGGL(reas_keys_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, pkts, stride,
+                           lens, n, now, G, groups, keys);
+    }
+    hipLaunchKernelGGL((reas_kernel<U>), dim3(groups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G,
+                       (const GroupKeys *)keys);
     return hipGetLastError();
 }
 

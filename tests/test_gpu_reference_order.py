@@ -217,7 +217,7 @@ def test_large_events_shuffled_with_duplicates(hip):
     got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, len(ln) // 3, len(ln)], "fused")
     assert st == rst and sorted(got) == sorted(ref)
     for k in ref:
-        assert [b for b, _ in got[k]] == ref[k]
+        assert sorted(got[k]) == sorted(ref[k])              # bytes and numFragments
     assert lost == rlost and loss == rloss
 
 
@@ -264,8 +264,10 @@ def test_reference_order_in_a_replayed_graph(hip):
     torch.cuda.synchronize()
     first = {}
     for rec in R.poll():
-        first.setdefault((rec.eventNum, rec.dataId), []).append(R.event_bytes(rec))
-    assert {k: sorted(v) for k, v in first.items()} == {k: sorted(v) for k, v in ref.items()}
+        first.setdefault((rec.eventNum, rec.dataId), []).append((R.event_bytes(rec), rec.numFragments))
+    assert sorted(first) == sorted(ref)
+    for k in ref:
+        assert sorted(first[k]) == sorted(ref[k]), k                 # bytes and numFragments
     graph = torch.cuda.CUDAGraph()
     with torch.cuda.graph(graph, stream=cap):
         body(cap)
@@ -274,7 +276,7 @@ def test_reference_order_in_a_replayed_graph(hip):
         torch.cuda.synchronize()
         got = {}
         for rec in R.poll():
-            got.setdefault((rec.eventNum, rec.dataId), []).append(R.event_bytes(rec))
+            got.setdefault((rec.eventNum, rec.dataId), []).append((R.event_bytes(rec), rec.numFragments))
         assert sorted(got) == sorted(ref), f"replay {replay}"
         for k in ref:
             assert sorted(got[k]) == sorted(ref[k]), (k, replay)

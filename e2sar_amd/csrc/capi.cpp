@@ -108,7 +108,7 @@ static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 // Group-key pre-pass in front of the fused kernel (reas_keys_kernel; build knob, A/B in
 // DESIGN.md 4.5)
 #ifndef E2SAR_REAS_PREPASS
-#define E2SAR_REAS_PREPASS 1
+#define E2SAR_REAS_PREPASS 0
 #endif
 
 // Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
@@ -1061,13 +1061,14 @@ int e2sar_hip_route_append(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32_
     if (capPerRank == 0 || (uint64_t)capPerRank * world > 0xFFFFFFFFull)
         return fail(E2SAR_HIP_ERR_PARAMETER, "capPerRank must be > 0 and capPerRank * world < 2^32");
     if (!d_running) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL running counters");
-    if (nPackets && (!d_packets || !d_lens || !d_sendPackets || !d_sendLens || !d_workspace))
+    if (nPackets && (!d_packets || !d_lens || !d_sendPackets || !d_sendLens))
         return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
-    if (workspaceBytes < route_workspace_bytes(nPackets, world)) return fail(E2SAR_HIP_ERR_PARAMETER, "workspace too small");
+    (void)d_workspace;
+    (void)workspaceBytes;                  // one launch, no workspace (kept in the signature for callers)
     HIP_TRY(hipSetDevice(ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
-    hipError_t e = launch_route(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, foreignOnly ? 1 : 0,
-                                d_sendPackets, d_sendLens, nullptr, d_workspace, s, capPerRank, d_running);
+    hipError_t e = launch_route_append(d_packets, stride, d_lens, nPackets, withLBHeader, world, self, foreignOnly ? 1 : 0,
+                                       d_sendPackets, d_sendLens, capPerRank, d_running, s);
     if (e != hipSuccess) return hip_fail(e, "route launch");
     return E2SAR_HIP_OK;
 }

@@ -1308,10 +1308,11 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
 }
 
 // Scatter stores: 1 = destination-aligned (shift_store: source-aligned loads, the next
-// chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 0 = source-aligned
-// chunks stored at their misaligned destination (scatter_chunk), the round-2 form.
+// chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 2 = the same with
+// every lane loading its chunk pair itself; 0 = source-aligned chunks stored at their
+// misaligned destination (scatter_chunk), the round-2 form.
 #ifndef E2SAR_SCATTER_SHIFT
-#define E2SAR_SCATTER_SHIFT 1
+#define E2SAR_SCATTER_SHIFT 0
 #endif
 
 // Bytes [s, s+16) of the 32-byte register pair lo:hi (s in 0..15, lane-varying): a funnel
@@ -1403,7 +1404,8 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
             const uint8_t *src = bpk + (uint64_t)p * stride + 16u * cc[u];
             x[u] = NT ? ld16_nt(src) : ld16(src);
             xn[u] = u32x4{0u, 0u, 0u, 0u};
-            if (E2SAR_SCATTER_SHIFT && last && cc[u] + 1u < spc) xn[u] = NT ? ld16_nt(src + 16) : ld16(src + 16);
+            if ((E2SAR_SCATTER_SHIFT == 2 || (E2SAR_SCATTER_SHIFT == 1 && last)) && cc[u] + 1u < spc)
+                xn[u] = NT ? ld16_nt(src + 16) : ld16(src + 16);
         }
     };
     issue(0);
@@ -1427,7 +1429,10 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
         for (int u = 0; u < U; u++) {
             // next chunk from lane + 1 (whole wave active: DPP reads every lane)
             const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
-#if E2SAR_SCATTER_SHIFT
+#if E2SAR_SCATTER_SHIFT == 2
+            if (i >= nch) continue;
+            shift_store(sinfo[pp[u]], cc[u], x[u], xn[u]);          // every lane loaded its pair
+#elif E2SAR_SCATTER_SHIFT == 1
             u32x4 nx;
             nx.x = lane_next(x[u].x, 0u);
             nx.y = lane_next(x[u].y, 0u);
@@ -2412,6 +2417,95 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
             }
         }
     }
+}
+
+// Append routing in ONE launch (e2sar_hip_route_append): a workgroup of 256 datagrams counts
+// its datagrams per destination (wave ballots), reserves room in each destination's region
+// with one atomicAdd on that region's counter, and copies its datagrams there -- no
+// histogram / scan launches in front of the copy (three dependent launches cost ~20 us per
+// batch even when nothing is foreign).  Within a workgroup a destination's datagrams keep
+// their order; workgroups append in the order they reserve.
+__global__ __launch_bounds__(kBlock) void route_append_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                              const uint32_t *__restrict__ lens, uint32_t n, int withLB,
+                                                              uint32_t world, uint32_t self, int excludeSelf, uint32_t cap,
+                                                              uint32_t *__restrict__ running, uint8_t *__restrict__ out,
+                                                              uint32_t *__restrict__ outLens)
+{
+    __shared__ uint32_t pos[kBlock];
+    __shared__ uint32_t waveCnt[kBlock / 64][kMaxWorld];
+    __shared__ uint32_t base[kMaxWorld];
+    const uint32_t p = blockIdx.x * kBlock + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const uint32_t dest = route_dest_x(pkts, stride, lens, p, n, withLB, world, self, excludeSelf);
+    uint32_t rank = 0;
+    for (uint32_t d = 0; d < world; d++) {
+        const uint64_t m = __ballot(dest == d);
+        if (dest == d) rank = (uint32_t)__builtin_popcountll(m & ((1ull << lane) - 1ull));
+        if (lane == 0) waveCnt[wv][d] = (uint32_t)__builtin_popcountll(m);
+    }
+    __syncthreads();
+    if (threadIdx.x < world) {
+        uint32_t tot = 0;
+        for (uint32_t w = 0; w < kBlock / 64; w++) tot += waveCnt[w][threadIdx.x];
+        base[threadIdx.x] = tot ? atomicAdd(&running[threadIdx.x], tot) : 0u;
+    }
+    __syncthreads();
+    uint32_t q = kNoDest;
+    if (dest != kNoDest) {
+        uint32_t before = 0;
+        for (uint32_t w = 0; w < wv; w++) before += waveCnt[w][dest];
+        const uint32_t r = base[dest] + before + rank;
+        if (r < cap) {                                        // nothing past the region; running still counts it
+            q = dest * cap + r;
+            outLens[q] = lens[p];
+        }
+    }
+    pos[threadIdx.x] = q;
+    if (!__syncthreads_or(q != kNoDest)) return;
+    const uint32_t p0 = blockIdx.x * kBlock;
+    const uint32_t np = (n - p0 < kBlock) ? n - p0 : kBlock;
+    const uint32_t spc = stride >> 4;
+    const uint32_t nch = np * spc;
+    const float rspc = 1.0f / (float)spc;
+    constexpr int UR = 4;
+    for (uint32_t r0 = 0; r0 < nch; r0 += kBlock * UR) {
+        u32x4 x[UR];
+        uint32_t qq[UR], cc[UR];
+#pragma unroll
+        for (int u = 0; u < UR; u++) {
+            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            const uint32_t ic = (i < nch) ? i : 0u;
+            uint32_t k = (uint32_t)((float)ic * rspc);
+            if (k * spc > ic) k--;
+            else if ((k + 1u) * spc <= ic) k++;
+            cc[u] = ic - k * spc;
+            qq[u] = (i < nch) ? pos[k] : kNoDest;
+            x[u] = u32x4{0u, 0u, 0u, 0u};
+            if (qq[u] != kNoDest)
+                x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
+                                             : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < UR; u++) {
+            if (qq[u] != kNoDest) {
+                uint8_t *o = out + (uint64_t)qq[u] * stride + 16u * cc[u];
+                if (E2SAR_PACK_POL & 1) st16_nt(o, x[u]);
+                else st16(o, x[u]);
+            }
+        }
+    }
+}
+
+hipError_t launch_route_append(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
+                               uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
+                               uint32_t cap, uint32_t *running, hipStream_t stream)
+{
+    if (world == 0 || world > kMaxWorld || self >= world || cap == 0) return hipErrorInvalidValue;
+    if ((uint64_t)cap * world > 0xFFFFFFFFull) return hipErrorInvalidValue;
+    if (n == 0) return hipSuccess;
+    hipLaunchKernelGGL(route_append_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, pkts, stride, lens, n, withLB,
+                       world, self, excludeSelf, cap, running, out, outLens);
+    return hipGetLastError();
 }
 
 size_t route_workspace_bytes(uint32_t n, uint32_t world)

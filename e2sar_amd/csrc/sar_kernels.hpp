@@ -226,6 +226,11 @@ hipError_t launch_recycle(const ReasDev &R, bool dropCompleted, hipStream_t stre
 // table/arena (same ctl), then make `to`'s top and slot count current.
 hipError_t launch_compact(const ReasDev &from, const ReasDev &to, hipStream_t stream);
 size_t route_workspace_bytes(uint32_t n, uint32_t world);
+// one launch: reserve per-workgroup room in each destination's region (atomicAdd on
+// running[d]) and copy; datagrams past a region's cap are counted, not written
+hipError_t launch_route_append(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
+                               uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
+                               uint32_t cap, uint32_t *running, hipStream_t stream);
 hipError_t launch_route(const uint8_t *pkts, uint32_t stride, const uint32_t *lens, uint32_t n, int withLB,
                         uint32_t world, uint32_t self, int excludeSelf, uint8_t *out, uint32_t *outLens,
                         uint32_t *counts, void *workspace, hipStream_t stream, uint32_t cap = 0,

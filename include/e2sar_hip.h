@@ -397,10 +397,15 @@ int e2sar_hip_route_foreign(e2sar_hip_ctx *ctx, const uint8_t *d_packets, uint32
                             size_t workspaceBytes, void *stream);
 
 /* Per-batch routing into per-rank regions, for a stream of landed batches exchanged once
- * per step: rank d's datagrams go to slots [d*capPerRank + running[d], ...) of
- * d_sendPackets / d_sendLens (stable order, appended after the earlier batches'), and
+ * per step: rank d's datagrams are appended to region d -- slots [d*capPerRank,
+ * (d+1)*capPerRank) of d_sendPackets / d_sendLens -- after the ones already there, and
  * running[d] (device, world counters, zeroed by the caller before the first batch, e.g.
- * e2sar_hip_memset_d) grows by this batch's count for d.  A datagram that would land past
+ * e2sar_hip_memset_d) grows by this batch's count for d.  One launch: each workgroup of 256
+ * datagrams reserves its room with one atomic per destination, so within a batch the order
+ * of a destination's datagrams is kept inside each 256-datagram block, and the blocks
+ * append in the order they reserve (the order-insensitive reassembler does not care; a
+ * REFERENCE_ORDER receiver takes the region order as the arrival order).  The workspace
+ * arguments are unused (NULL / 0 allowed).  A datagram that would land past
  * its region is not written, but still counted: running[d] > capPerRank after the step
  * means the regions were too small.  foreignOnly: as e2sar_hip_route_foreign (this rank's
  * datagrams and unparsable ones stay here, running[self] stays 0).  Routing each batch

@@ -255,9 +255,12 @@ def _pmc_traffic(args, dom):
         w = pmc.get("workload") or {}
         if (w.get("mtu") == args.mtu and w.get("event_bytes") == args.event_bytes
                 and w.get("batch_events") == args.batch_events and w.get("lb_version", 2) == args.lb_version):
-            for k, v in (pmc.get("kernels") or {}).items():
-                if k.split("<")[0] == dom:
-                    return int(v["hbm_bytes_per_launch"]), pmc.get("file", os.path.relpath(path, ROOT))
+            ks = pmc.get("kernels") or {}
+            # reassemble_batch's split form (batches above 320 MiB of slots) is two launches
+            parts = ("reas_classify_kernel", "reas_scatter_kernel") if dom == "reassemble_batch_split" else (dom,)
+            got = [v for p in parts for k, v in ks.items() if k.split("<")[0] == p]
+            if len(got) == len(parts):
+                return int(sum(v["hbm_bytes_per_launch"] for v in got)), pmc.get("file", os.path.relpath(path, ROOT))
     return None, None
 
 

@@ -40,6 +40,10 @@ def main():
     ap.add_argument("--slots", type=int, default=3)
     ap.add_argument("--only", choices=["recv", "send", "both", "relay"], default=None,
                     help="time one mode only (for tracing)")
+    ap.add_argument("--copy", choices=["dma", "kernel-d2h", "kernel"], default="dma",
+                    help="dma: hipMemcpyAsync for both directions; kernel-d2h: device->host copies by "
+                         "e2sar_hip_copy_spans (the GPU stores into pinned host memory); kernel: both "
+                         "directions by copy_spans (the GPU loads from / stores to pinned host memory)")
     args = ap.parse_args()
 
     import torch
@@ -87,13 +91,28 @@ def main():
     rs = [torch.cuda.Stream() for _ in range(2)]      # recv: H2D + kernel, D2H
     ss = [torch.cuda.Stream() for _ in range(2)]      # send: H2D + kernel, D2H
 
+    def h2d(dst, src):
+        """host -> device copy on the current stream (DMA or a copy_spans kernel)."""
+        if args.copy == "kernel":
+            ctx.copy_spans([(src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size())],
+                           stream=torch.cuda.current_stream())
+        else:
+            dst.copy_(src, non_blocking=True)
+
+    def d2h(dst, src):
+        if args.copy in ("kernel", "kernel-d2h"):
+            ctx.copy_spans([(src.data_ptr(), dst.data_ptr(), src.numel() * src.element_size())],
+                           stream=torch.cuda.current_stream())
+        else:
+            dst.copy_(src, non_blocking=True)
+
     def recv_batch(k, ev_done):
         s = k % S
         with torch.cuda.stream(rs[0]):
             if ev_done[s] is not None:
                 rs[0].wait_event(ev_done[s])
-            d_pk[s].copy_(h_pk[s], non_blocking=True)
-            d_ln[s].copy_(h_ln[s], non_blocking=True)
+            h2d(d_pk[s], h_pk[s])
+            h2d(d_ln[s], h_ln[s])
             R[s].recycle(force=True, stream=rs[0])    # events of this batch fill arena[0, BE*ev_stride)
             R[s].reassemble(d_pk[s], stride, d_ln[s], bpk, stream=rs[0])
             e1 = torch.cuda.Event()
@@ -101,7 +120,7 @@ def main():
         rs[1].wait_event(e1)
         with torch.cuda.stream(rs[1]):
             # the batch's events fill the recycled arena contiguously (256-B aligned buffers)
-            h_out_events[s].view(-1).copy_(arena_views[s], non_blocking=True)
+            d2h(h_out_events[s].view(-1), arena_views[s])
             e2 = torch.cuda.Event()
             e2.record(rs[1])
         ev_done[s] = e2
@@ -111,13 +130,13 @@ def main():
         with torch.cuda.stream(ss[0]):
             if ev_done[s] is not None:
                 ss[0].wait_event(ev_done[s])
-            d_ev[s].copy_(h_events[s], non_blocking=True)
+            h2d(d_ev[s], h_events[s])
             seg.segment(plans[s], d_spk[s][0], d_spk[s][1], stream=ss[0])
             e1 = torch.cuda.Event()
             e1.record(ss[0])
         ss[1].wait_event(e1)
         with torch.cuda.stream(ss[1]):
-            h_out_pk[s].copy_(d_spk[s][0][: bpk * stride], non_blocking=True)
+            d2h(h_out_pk[s], d_spk[s][0][: bpk * stride])
             e2 = torch.cuda.Event()
             e2.record(ss[1])
         ev_done[s] = e2
@@ -132,8 +151,8 @@ def main():
         with torch.cuda.stream(rs[0]):
             if ev_done[s] is not None:
                 rs[0].wait_event(ev_done[s])
-            d_pk[s].copy_(h_pk[s], non_blocking=True)
-            d_ln[s].copy_(h_ln[s], non_blocking=True)
+            h2d(d_pk[s], h_pk[s])
+            h2d(d_ln[s], h_ln[s])
             R[s].recycle(force=True, stream=rs[0])
             R[s].reassemble(d_pk[s], stride, d_ln[s], bpk, stream=rs[0])
             R[s].relay_plan(relay_desc[s], relay_cnt[s], 0, BE, seg.max_pld, 7 + k, 1 + k, stream=rs[0])
@@ -149,7 +168,7 @@ def main():
         total = int(relay_hcnt[s][1])
         rs[1].wait_event(ev_cnt[s])
         with torch.cuda.stream(rs[1]):
-            h_out_pk[s][: total * stride].copy_(d_spk[s][0][: total * stride], non_blocking=True)
+            d2h(h_out_pk[s][: total * stride], d_spk[s][0][: total * stride])
             e2 = torch.cuda.Event()
             e2.record(rs[1])
         ev_done[s] = e2
@@ -189,7 +208,7 @@ def main():
         assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], dev_events[r.eventNum, :B])
 
     res = {"config": f"host path: {BE} x {B} B events per batch, MTU {args.mtu}, pinned buffers, "
-                     f"2 streams per direction (H2D+kernel, D2H), {S} rotating buffer sets"}
+                     f"2 streams per direction (H2D+kernel, D2H), {S} rotating buffer sets, copies: {args.copy}"}
     if args.only:
         res[args.only + "_GiBps"] = round(run(args.only), 2)
         print(json.dumps(res), flush=True)
@@ -224,6 +243,16 @@ def main():
             h_out_pk[k % S].copy_(d_spk[k % S][0][: bpk * stride], non_blocking=True)
     torch.cuda.synchronize()
     res["pcie_bidir_GBps_each"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
+    # the same with copy_spans kernels (the GPU's own loads / stores across PCIe)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.batches):
+        with torch.cuda.stream(rs[0]):
+            ctx.copy_spans([(h_pk[k % S].data_ptr(), d_pk[k % S].data_ptr(), bpk * stride)], stream=rs[0])
+        with torch.cuda.stream(rs[1]):
+            ctx.copy_spans([(d_spk[k % S][0].data_ptr(), h_out_pk[k % S].data_ptr(), bpk * stride)], stream=rs[1])
+    torch.cuda.synchronize()
+    res["pcie_bidir_kernel_GBps_each"] = round(args.batches * bpk * stride / (time.perf_counter() - t0) / 1e9, 1)
     print(json.dumps(res), flush=True)
 
 

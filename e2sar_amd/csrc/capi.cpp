@@ -110,10 +110,6 @@ static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 #ifndef E2SAR_REAS_PREPASS
 #define E2SAR_REAS_PREPASS 0
 #endif
-// reassemble_batch's split form takes the batch from its end (build knob, A/B in DESIGN.md 4.5)
-#ifndef E2SAR_SPLIT_REVERSE
-#define E2SAR_SPLIT_REVERSE 1
-#endif
 
 // Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
 // cold (E2SAR_HIP_REAS_COLD_DATAGRAMS), and for a batch too large to still be cached.
@@ -609,12 +605,8 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     // of this stream, grown on first use (outside graph capture).
     if ((uint64_t)nPackets * stride > kFusedMaxBytes) {
         if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, work_bytes(nPackets))) return rc;
-        // both launches take the batch from its end: its last datagrams are the ones a
-        // segmentation or receive that just wrote it in order left in the Infinity Cache
-        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork, s,
-                                            E2SAR_SPLIT_REVERSE != 0);
-        if (e == hipSuccess)
-            e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, true, E2SAR_SPLIT_REVERSE != 0);
+        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, true);
         if (e == hipSuccess) e = note_launch(r, s);
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;

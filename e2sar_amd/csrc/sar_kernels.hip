@@ -48,9 +48,6 @@ constexpr int kBlock = 256;
 // GiB/s, 3 1414, 4 1399-1404, 6 1397, 8 1362, 1 1341; 1 MiB at MTU 9000, U = 2 1434 vs 4
 // 1418; 8 MiB at MTU 9000 (32 per launch), U = 2 1325-1334 vs 4 1362-1371.  E2SAR_SEG_U
 // (env, 2 or 4) overrides.
-#ifndef E2SAR_FUSED_REVERSE
-#define E2SAR_FUSED_REVERSE 0       // reas_kernel groups from the batch's end (A/B)
-#endif
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
@@ -1158,10 +1155,7 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(Reas
                                                                            const GroupKeys *__restrict__ keys)
 {
     __shared__ ReasGroupLds L;
-    // E2SAR_FUSED_REVERSE (A/B): groups from the batch's end, where the datagrams written
-    // last are the likeliest to still be in the Infinity Cache
-    reas_group<U>(R, pkts, stride, lens, n, now, G, E2SAR_FUSED_REVERSE ? gridDim.x - 1u - blockIdx.x : blockIdx.x, L,
-                  keys);
+    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys);
 }
 
 // Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
@@ -1465,21 +1459,19 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,
                                                                uint32_t n, uint64_t now, PktInfo *__restrict__ info,
-                                                               FinishRec *__restrict__ fin, uint32_t reverse)
+                                                               FinishRec *__restrict__ fin)
 {
-    // reverse: the last datagrams of the batch first (see launch_reas_scatter)
-    const uint32_t blk = reverse ? gridDim.x - 1u - blockIdx.x : blockIdx.x;
-    classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blk * (kBlock / 64) + (threadIdx.x >> 6));
+    classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
 template <int U, bool NT>
 __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t n, uint32_t G,
                                                               const PktInfo *__restrict__ info,
-                                                              const FinishRec *__restrict__ fin, uint32_t reverse)
+                                                              const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, reverse ? gridDim.x - 1u - blockIdx.x : blockIdx.x, sinfo);
+    scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
@@ -2135,22 +2127,17 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
 }
 
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
-                                uint32_t n, uint64_t now, void *work, hipStream_t stream, bool reverse)
+                                uint32_t n, uint64_t now, void *work, hipStream_t stream)
 {
     if (n == 0) return hipSuccess;
     uint8_t *w = static_cast<uint8_t *>(work);
     hipLaunchKernelGGL(reas_classify_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens,
-                       n, now, reinterpret_cast<PktInfo *>(w), reinterpret_cast<FinishRec *>(w + work_fin_off(n)),
-                       reverse ? 1u : 0u);
+                       n, now, reinterpret_cast<PktInfo *>(w), reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
 
-// reverse: workgroups take the batch from its end.  For a batch larger than the Infinity
-// Cache that was just written in order (reassemble_batch's split form), the datagrams
-// written last are the ones still cached, and the first wave of workgroups reads those
-// before later traffic evicts them.
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
-                               const void *work, hipStream_t stream, bool nt, bool reverse)
+                               const void *work, hipStream_t stream, bool nt)
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
@@ -2158,12 +2145,10 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const uint32_t G = scatter_group_size(stride);
     if (nt)
         hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
-                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)),
-                           reverse ? 1u : 0u);
+                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     else
         hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
-                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)),
-                           reverse ? 1u : 0u);
+                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
 

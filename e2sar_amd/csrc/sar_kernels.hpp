@@ -212,10 +212,9 @@ struct ChainBatches {
 hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint32_t stride, const ReasDev &R,
                           uint64_t now, hipStream_t stream);
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
-                                uint32_t n, uint64_t now, void *work, hipStream_t stream, bool reverse = false);
+                                uint32_t n, uint64_t now, void *work, hipStream_t stream);
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
-                               const void *work, hipStream_t stream, bool nt,   // nt: streaming datagram loads
-                               bool reverse = false);                           // workgroups from the batch's end
+                               const void *work, hipStream_t stream, bool nt);   // nt: streaming datagram loads
 hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const uint8_t *spk, uint32_t sn,
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
                                         uint64_t now, void *cwork, hipStream_t stream, bool nt);

@@ -1,4 +1,4 @@
-"""every C++ snippet compiles against include/e2sar_hip.h.
+"""INTEGRATION.md sections 3 and 4: every C++ snippet compiles against include/e2sar_hip.h.
 
 The snippets are what a maintainer would paste into the reference (its SendThreadState::
 _send, its receive body, its pybind module); the reference's own EventQueueItem and
@@ -20,10 +20,10 @@ void enqueue(EventQueueItem *item);
 """
 
 
-def _snippets():
+def _snippets(section="## 3.", end="## 4."):
     with open(os.path.join(ROOT, "INTEGRATION.md")) as f:
         text = f.read()
-    sec = text[text.index("## 3."):text.index("## 4.")]
+    sec = text[text.index(section):(text.index(end) if end else len(text))]
     return re.findall(r"```cpp\n(.*?)```", sec, re.S)
 
 
@@ -33,9 +33,12 @@ def test_integration_has_the_three_seams():
     assert "e2sar_hip_seg_plan(&ev, 1, maxPldLen, &n, &maxPk)" in snips[0]
 
 
-@pytest.mark.parametrize("k", range(3))
+ALL = _snippets() + _snippets("## 4.", None)
+
+
+@pytest.mark.parametrize("k", range(len(ALL)))
 def test_integration_snippet_compiles(tmp_path, k):
-    code = _snippets()[k]
+    code = ALL[k]
     src = tmp_path / f"snippet{k}.cpp"
     src.write_text(PRELUDE + code)
     cmd = ["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror", "-Wno-unused-function",

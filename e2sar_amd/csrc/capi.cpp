@@ -110,10 +110,6 @@ static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 #ifndef E2SAR_REAS_PREPASS
 #define E2SAR_REAS_PREPASS 0
 #endif
-// reassemble_batch's split form (batches above kFusedMaxBytes): parts pipelined per launch
-#ifndef E2SAR_SPLIT_PARTS
-#define E2SAR_SPLIT_PARTS 2
-#endif
 
 // Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
 // cold (E2SAR_HIP_REAS_COLD_DATAGRAMS), and for a batch too large to still be cached.
@@ -608,26 +604,9 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     // datagrams, BASELINE config 3): 1116 GiB/s fused vs 1302 split.  Internal work buffer
     // of this stream, grown on first use (outside graph capture).
     if ((uint64_t)nPackets * stride > kFusedMaxBytes) {
-        // E2SAR_SPLIT_PARTS > 1: the batch in that many consecutive parts, pipelined as
-        // classify(0), [scatter(k) | classify(k+1)], ..., scatter(last), so only the first
-        // part's classification (a latency-bound launch) sits in front of the copy
-        const uint32_t parts = std::max<uint32_t>(1u, std::min<uint32_t>(E2SAR_SPLIT_PARTS, nPackets));
-        std::vector<uint32_t> cut(parts + 1);
-        for (uint32_t k = 0; k <= parts; k++) cut[k] = (uint32_t)((uint64_t)nPackets * k / parts);
-        std::vector<size_t> woff(parts + 1, 0);
-        for (uint32_t k = 0; k < parts; k++) woff[k + 1] = woff[k] + ((work_bytes(cut[k + 1] - cut[k]) + 255) & ~(size_t)255);
-        if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, woff[parts])) return rc;
-        auto *wb = static_cast<uint8_t *>(sc.roWork);
-        auto pk = [&](uint32_t k) { return d_packets + (size_t)cut[k] * stride; };
-        hipError_t e = launch_reas_classify(r->dev, pk(0), stride, d_lens, cut[1], now_ms, wb, s);
-        for (uint32_t k = 0; e == hipSuccess && k < parts; k++) {
-            if (k + 1 < parts)
-                e = launch_reas_scatter_classify(r->dev, stride, pk(k), cut[k + 1] - cut[k], wb + woff[k], pk(k + 1),
-                                                 d_lens + cut[k + 1], cut[k + 2] - cut[k + 1], now_ms, wb + woff[k + 1],
-                                                 s, true);
-            else
-                e = launch_reas_scatter(r->dev, pk(k), stride, cut[k + 1] - cut[k], wb + woff[k], s, true);
-        }
+        if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, work_bytes(nPackets))) return rc;
+        hipError_t e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork, s);
+        if (e == hipSuccess) e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, true);
         if (e == hipSuccess) e = note_launch(r, s);
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;

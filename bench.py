@@ -75,6 +75,8 @@ def parse(argv=None):
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
+    ap.add_argument("--spread-eager", action="store_true",
+                    help="spread landing: launch the landing part eagerly too (default: one HIP graph per step)")
     ap.add_argument("--table-factor", type=int, default=8,
                     help="event-table slots = next power of two >= factor x events per step")
     ap.add_argument("--cold-steps", type=int, default=10,
@@ -485,16 +487,30 @@ def run_workload(args, env, headline: bool):
     last_counts = []
     last_recv = [0]
 
-    def step_spread():
-        """Datagrams land on this rank whatever their owner: this rank's events are
-        reassembled in place (hot), the foreign ones routed, exchanged (RCCL all-to-all-v)
-        and reassembled by their owners."""
+    def spread_landed():
+        """The device part of a spread-landing step (capturable): every batch lands, this
+        rank's events are reassembled in place (hot), the foreign datagrams appended to the
+        per-owner regions."""
         lpk, lln = land
+        R.recycle(force=True)
         router.reset()
         for p in plans:
             timed("seg_kernel", seg.segment, p, lpk, lln)
             timed("reas_kernel", R.reassemble, lpk, stride, lln, p.total_packets)
             timed("route_kernels", router.route, lpk, lln, p.total_packets)
+
+    spread_graph = [None]
+
+    def step_spread():
+        """Datagrams land on this rank whatever their owner: this rank's events are
+        reassembled in place (hot), the foreign ones routed, exchanged (RCCL all-to-all-v)
+        and reassembled by their owners.  The landing part replays as a HIP graph once
+        captured (not in the per-kernel timing pass); the exchange needs a host read of the
+        split sizes, so it and the received datagrams' reassembly run eagerly."""
+        if spread_graph[0] is not None and not timing_on[0]:
+            spread_graph[0].replay()
+        else:
+            spread_landed()
         if world > 1:
             rpk, rln, n = timed("exchange", router.exchange, out=recv_bufs)
             last_counts[:] = [int(c) for c in router.running.tolist()]
@@ -523,9 +539,9 @@ def run_workload(args, env, headline: bool):
         With --overlap, reassembly of batch b runs on a second stream concurrently with
         segmentation of batch b+1 (double-buffered datagram slots)."""
         s0 = torch.cuda.current_stream()
-        R.recycle(force=True)
         if spread:
             return step_spread()
+        R.recycle(force=True)
         if args.reas == "pipelined":
             # seg(0), classify(0); then per batch: seg(b+1), [scatter(b) | classify(b+1)]
             # in one launch; buffers b%2 are rewritten by seg(b+2) after that launch.
@@ -650,6 +666,12 @@ def run_workload(args, env, headline: bool):
         graph = capture(step, G)
         if not args.no_verify:
             verified = verify() and verified is not False
+    elif spread and not args.spread_eager:
+        spread_graph[0] = capture(spread_landed, 1)
+        step()
+        torch.cuda.synchronize()
+        if not args.no_verify:
+            verified = verify_spread() and verified is not False
 
     def run_timed(fn, g, k):
         """k steps (k/G graph replays, or k eager steps) between barriers; max over ranks."""
@@ -846,7 +868,10 @@ def run_workload(args, env, headline: bool):
                 "parallelism": (f"eventNum % {world} sharding (no collective)" if not spread else
                                 f"eventNum % {world} owners, datagrams land spread: route + all-to-all-v "
                                 f"({backend}) + reassemble"),
-                "launch": "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times",
+                "launch": ("landing part (segment, in-place reassembly, route) as one hipGraph per step; "
+                           "count read, exchange and received-datagram reassembly eager"
+                           if spread and spread_graph[0] is not None else
+                           "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times"),
                 "overlap": bool(args.overlap),
                 "reassembly": {"fused": ("reas_kernel per batch" if fused_name == "reas_kernel" else
                                          "reassemble_batch per batch, REFERENCE_ORDER: key pass, radix sort, "

@@ -147,6 +147,7 @@ SIGNATURES = {
     "e2sar_hip_memcpy_h2d": (i, [vp, vp, vp, sz]),
     "e2sar_hip_memcpy_d2h": (i, [vp, vp, vp, sz]),
     "e2sar_hip_memset_d": (i, [vp, vp, i, sz]),
+    "e2sar_hip_memset_async": (i, [vp, vp, i, sz, vp]),
     "e2sar_hip_memcpy_async": (i, [vp, vp, vp, sz, i, vp]),
     "e2sar_hip_stream_sync": (i, [vp, vp]),
     "e2sar_hip_event_create": (i, [vp, C.POINTER(vp)]),

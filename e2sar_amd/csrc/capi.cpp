@@ -283,6 +283,14 @@ int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes)
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_memset_async(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    HIP_TRY(hipSetDevice(ctx->device));
+    HIP_TRY(launch_fill_bytes(dst, value, bytes, stream ? static_cast<hipStream_t>(stream) : ctx->stream));
+    return E2SAR_HIP_OK;
+}
+
 int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind, void *stream)
 {
     if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");

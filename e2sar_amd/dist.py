@@ -171,11 +171,12 @@ class RegionRouter:
         ws = int(lib().e2sar_hip_route_workspace_bytes(max_batch, world))
         self.workspace = torch.empty(max(ws, 16), dtype=torch.uint8, device=d)
 
-    def reset(self) -> None:
-        """Empty the regions (a fill kernel on the context stream: capture-safe)."""
+    def reset(self, stream: Optional[torch.cuda.Stream] = None) -> None:
+        """Empty the regions (a fill kernel on the stream, default the current one: capture-safe)."""
         from ._capi import check, lib
-        check(lib().e2sar_hip_memset_d(self.ctx.handle, C.c_void_p(self.running.data_ptr()), 0,
-                                        self.running.numel() * 4))
+        from .sar import _stream_handle
+        check(lib().e2sar_hip_memset_async(self.ctx.handle, C.c_void_p(self.running.data_ptr()), 0,
+                                           self.running.numel() * 4, C.c_void_p(_stream_handle(stream))))
 
     def route(self, pk: torch.Tensor, ln: torch.Tensor, n: int, stream: Optional[torch.cuda.Stream] = None):
         from ._capi import check, lib

@@ -74,6 +74,8 @@ int e2sar_hip_memcpy_d2h(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t 
  * hipMemsetAsync, so the call may be captured into a HIP graph (captured memset nodes write
  * garbage from the second replay on with this ROCm) */
 int e2sar_hip_memset_d(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes);
+/* e2sar_hip_memset_d on `stream` (NULL = context stream): a fill kernel, capture-safe */
+int e2sar_hip_memset_async(e2sar_hip_ctx *ctx, void *dst, int value, size_t bytes, void *stream);
 /* asynchronous copy on `stream` (NULL = context stream); kind 0 = H2D, 1 = D2H, 2 = D2D */
 int e2sar_hip_memcpy_async(e2sar_hip_ctx *ctx, void *dst, const void *src, size_t bytes, int kind,
                            void *stream);

@@ -191,8 +191,13 @@ def _nccl_worker(port, result_q):
         rr.route(spk2, sln2, n // 2)
         rr.route(spk2[(n // 2) * stride:], sln2[n // 2:], n - n // 2)
         rpk2, rln2, nr2 = rr.exchange()
-        out["regions_raw"] = bool(nr2 == n and torch.equal(rpk2[: n * stride], spk2[: n * stride])
-                                  and torch.equal(rln2[:n], sln2))
+        # route_append keeps the order inside each 256-datagram workgroup only (workgroups
+        # append in the order they reserve): compare the received slots as a multiset, each
+        # slot with its length
+        got = torch.cat([rpk2[: n * stride].view(n, stride), rln2[:n].view(n, 1).to(torch.uint8)], 1).cpu()
+        want = torch.cat([spk2[: n * stride].view(n, stride), sln2.view(n, 1).to(torch.uint8)], 1).cpu()
+        key = lambda t: sorted(bytes(r.numpy()) for r in t)
+        out["regions_raw"] = bool(nr2 == n and key(got) == key(want) and torch.equal(rln2[:n], sln2))
         out["backend"] = dist.get_backend()
     finally:
         dist.destroy_process_group()

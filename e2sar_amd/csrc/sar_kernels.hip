@@ -117,9 +117,6 @@ __device__ __forceinline__ u32x4 ld16_nt(const uint8_t *p)
 __device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4 *)(p)); }
 // 16-byte store at a dword-aligned (not 16-byte-aligned) address (non-temporal unless
 // E2SAR_REAS_NT_STORE=0)
-#ifndef E2SAR_FUSED_NT_STORE
-#define E2SAR_FUSED_NT_STORE 1      // reas_kernel's aligned event stores non-temporal (A/B)
-#endif
 #ifndef E2SAR_REAS_NT_STORE
 #define E2SAR_REAS_NT_STORE 1
 #endif
@@ -977,11 +974,7 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
         (void)da_window(c, a, pi.hl, stride, sh);
         const u32x4 o = rot_down(x, sh >> 2);
         if (lo == 0u && hi == 16u) {
-#if E2SAR_FUSED_NT_STORE
             st16_nt(D, o);
-#else
-            st16(D, o);
-#endif
         } else {
 #pragma unroll
             for (uint32_t d = 0; d < 4; d++)

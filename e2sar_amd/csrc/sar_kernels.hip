@@ -288,34 +288,42 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 #ifndef E2SAR_SEG_BLOCK
 #define E2SAR_SEG_BLOCK 256         // seg_kernel threads per workgroup (A/B knob)
 #endif
-template <int U, bool HO, int SB = kBlock>
-__device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict__ events, uint32_t blocksPerEvent,
-                                          int lbVersion, uint32_t maxPld, uint8_t *__restrict__ pkts, uint32_t stride,
-                                          uint32_t *__restrict__ lens, const uint32_t *__restrict__ dCount,
-                                          uint32_t blk, uint32_t tileG, uint32_t *__restrict__ tiles)
+// One round of a segmentation block: index-space chunks [j0, j0 + SB*U) of event ev,
+// bounded by jEnd (the event's chunk count, or the end of a local chained range).
+struct SegEv {
+    SegHdr h;
+    const uint8_t *data;
+    uint32_t pktBase, bytes, npk, spc, maxPld;
+    float rspc;
+    bool A4;
+};
+
+__device__ __forceinline__ SegEv seg_ev(const e2sar_hip_seg_event &ev, int lbVersion, uint32_t maxPld, uint32_t stride)
 {
-    TRACE_AT(1, 0, trace_now());
-    const uint32_t e = blk / blocksPerEvent;
-    const uint32_t bx = blk - e * blocksPerEvent;
-    if (dCount && e >= *dCount) return;
-    const e2sar_hip_seg_event ev = events[e];
-    const bool A4 = (((uintptr_t)ev.data | maxPld) & 3u) == 0u;
-    const uint32_t bytes = ev.bytes;
-    const uint32_t npk = (bytes + maxPld - 1u) / maxPld;
-    const uint32_t spc = stride >> 4;
-    const uint32_t nch = npk * spc;
-    const uint32_t j0 = bx * (uint32_t)(SB * U);
-    if (j0 >= nch) return;
-
     HdrWords hw;
-    lbre_words(hw, lbVersion, ev.entropy, ev.lbTick, ev.dataId, 0u, bytes, ev.eventNum);
-    const SegHdr h{hw.w[0], hw.w[1], hw.w[2], hw.w[3], hw.w[4], hw.w[6], hw.w[7], hw.w[8]};
-    uint8_t *const out = pkts + (uint64_t)ev.pktBase * stride;
-    const __amdgpu_buffer_rsrc_t outR = brsrc(out + 16ull * j0);        // HO stores only
-    (void)outR;
-    const uint8_t *const safe = reinterpret_cast<const uint8_t *>(events + e);   // >= 16 valid bytes
-    const float rspc = 1.0f / (float)spc;
+    lbre_words(hw, lbVersion, ev.entropy, ev.lbTick, ev.dataId, 0u, ev.bytes, ev.eventNum);
+    SegEv E;
+    E.h = SegHdr{hw.w[0], hw.w[1], hw.w[2], hw.w[3], hw.w[4], hw.w[6], hw.w[7], hw.w[8]};
+    E.data = ev.data;
+    E.pktBase = ev.pktBase;
+    E.bytes = ev.bytes;
+    E.npk = (ev.bytes + maxPld - 1u) / maxPld;
+    E.spc = stride >> 4;
+    E.maxPld = maxPld;
+    E.rspc = 1.0f / (float)E.spc;
+    E.A4 = (((uintptr_t)ev.data | maxPld) & 3u) == 0u;
+    return E;
+}
 
+template <int U, bool HO, int SB>
+__device__ __forceinline__ void seg_round(const SegEv &E, uint8_t *__restrict__ out, __amdgpu_buffer_rsrc_t outR,
+                                          uint32_t outJ0, const uint8_t *safe, uint32_t *__restrict__ lens,
+                                          uint32_t j0, uint32_t jEnd)
+{
+    const SegHdr h = E.h;        // a copy: a reference into E leaves E in scratch memory
+    const uint32_t bytes = E.bytes, npk = E.npk, spc = E.spc, maxPld = E.maxPld;
+    const bool A4 = E.A4;
+    const float rspc = E.rspc;
     u32x4 x[U];
     uint32_t jj[U], cc[U], LL[U], kk[U], sh[U];
     bool rare[U];
@@ -327,7 +335,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
         cc[u] = LL[u] = kk[u] = sh[u] = 0;
         rare[u] = false;
         const uint8_t *a = safe;
-        if (j < nch) {
+        if (j < jEnd) {
             // k = j / spc: a float reciprocal and a +-1 correction while k < 2^22 (the
             // estimate is then off by less than one); integer division for the datagrams of
             // larger events (npk is event-uniform, so the branch never diverges)
@@ -343,15 +351,15 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
             const uint32_t off = k * maxPld;
             const uint32_t L = (bytes - off > maxPld) ? maxPld : bytes - off;
             if (c == 0u && lens) {
-                if (HO) st4_sc1(lens + ev.pktBase + k, kLBREHdrLen + L);
-                else lens[ev.pktBase + k] = kLBREHdrLen + L;
+                if (HO) st4_sc1(lens + E.pktBase + k, kLBREHdrLen + L);
+                else lens[E.pktBase + k] = kLBREHdrLen + L;
             }
             if (16u * c < kLBREHdrLen + L) {          // else: chunk wholly past the datagram end
                 jj[u] = j;
                 cc[u] = c;
                 LL[u] = L;
                 kk[u] = k;
-                const uint8_t *pl = ev.data + off;
+                const uint8_t *pl = E.data + off;
                 if (!A4) {
                     rare[u] = true;
                 } else if (c >= 3u) {
@@ -374,7 +382,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
         if (jj[u] == 0xFFFFFFFFu) continue;
         const uint32_t c = cc[u], L = LL[u];
         const uint32_t w5 = bswap32(kk[u] * maxPld);
-        const uint8_t *pl = ev.data + kk[u] * maxPld;
+        const uint8_t *pl = E.data + kk[u] * maxPld;
         u32x4 o;
         if (rare[u]) {
             if (!A4) {
@@ -397,9 +405,32 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
         } else {
             o = u32x4{h.w0, h.w1, h.w2, h.w3};
         }
-        if (HO) st16_sc1(outR, 16u * (jj[u] - j0), o);
+        if (HO) st16_sc1(outR, 16u * (jj[u] - outJ0), o);
         else st16(out + 16u * jj[u], o);
     }
+}
+
+template <int U, bool HO, int SB = kBlock>
+__device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict__ events, uint32_t blocksPerEvent,
+                                          int lbVersion, uint32_t maxPld, uint8_t *__restrict__ pkts, uint32_t stride,
+                                          uint32_t *__restrict__ lens, const uint32_t *__restrict__ dCount,
+                                          uint32_t blk, uint32_t tileG, uint32_t *__restrict__ tiles)
+{
+    TRACE_AT(1, 0, trace_now());
+    const uint32_t e = blk / blocksPerEvent;
+    const uint32_t bx = blk - e * blocksPerEvent;
+    if (dCount && e >= *dCount) return;
+    const e2sar_hip_seg_event ev = events[e];
+    const SegEv E = seg_ev(ev, lbVersion, maxPld, stride);
+    const uint32_t spc = E.spc;
+    const uint32_t nch = E.npk * spc;
+    const uint32_t j0 = bx * (uint32_t)(SB * U);
+    if (j0 >= nch) return;
+
+    uint8_t *const out = pkts + (uint64_t)ev.pktBase * stride;
+    const __amdgpu_buffer_rsrc_t outR = brsrc(out + 16ull * j0);        // HO stores only
+    const uint8_t *const safe = reinterpret_cast<const uint8_t *>(events + e);   // >= 16 valid bytes
+    seg_round<U, HO, SB>(E, out, outR, j0, safe, lens, j0, nch);
     if (HO) {
         // every storing wave waits for its write-through stores, then one wave signals for
         // the workgroup behind the barrier
@@ -1009,20 +1040,18 @@ struct ReasGroupLds {
 // HO: the chained form -- every datagram byte and length is read with sc1 loads (they were
 // stored write-through by seg_block in the same launch).
 template <int U, bool HO = false>
-__device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
-                                           const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
-                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr)
+__device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                           const uint32_t *__restrict__ lens, uint32_t g0, uint32_t gn, uint64_t now,
+                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ key)
 {
     const uint32_t tx = threadIdx.x;
-    const uint32_t g0 = g * G;
-    const uint32_t gn = (n - g0 < G) ? n - g0 : G;
     const bool w0 = tx < 64;
     const uint32_t lane = tx & 63u;
 
     // the group's pre-resolved keys (scalar loads, issued first: they ride beside the
     // header loads instead of a dependent table round trip after them)
     GroupKeys K{};
-    if (keys) K = keys[g];
+    if (key) K = *key;
     TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
@@ -1080,7 +1109,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 
     unsigned long long old = 0;
     if (w0) {
-        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g, keys != nullptr, K);
+        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g, key != nullptr, K);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -1137,6 +1166,16 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     __syncthreads();
     TRACE_AT(0, 3, trace_now());
 #endif
+}
+
+template <int U, bool HO = false>
+__device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                           const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
+                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr)
+{
+    const uint32_t g0 = g * G;
+    const uint32_t gn = (n - g0 < G) ? n - g0 : G;
+    reas_range<U, HO>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
 }
 
 // reas_kernel: workgroup b reassembles datagrams [b*G, b*G + G) of the batch.

@@ -62,6 +62,14 @@ def parse(argv=None):
                     help="steps captured in one HIP graph (0: the largest of 4, 2, 1 that divides --steps); "
                          "the timed region still runs exactly --steps steps")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
+    ap.add_argument("--xcd-groups", type=int, default=0,
+                    help="1: reassemble each batch over the group table that matches seg_kernel's XCD stripes "
+                         "(e2sar_hip_seg_groups / e2sar_hip_reassemble_groups: every datagram read on the XCD "
+                         "that wrote it)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="independent segment -> reassemble pipelines on this many streams, batches dealt out "
+                         "round-robin, each lane with its own datagram buffer (so the datagrams resident at "
+                         "once stay lanes x batch): one lane's launch head and tail overlap another's body")
     ap.add_argument("--reas", choices=["fused", "split", "pipelined", "chained"], default="fused",
                     help="fused: one reassemble_batch launch per batch; split: classify + scatter launches "
                          "in line; pipelined: one launch scatters batch b while other workgroups classify "
@@ -269,15 +277,17 @@ def _pmc_traffic(args, dom):
 def copy_calibration(ctx, torch, dev):
     """Achievable HBM on this device beside the 8 TB/s peak: the best of
     device copies with e2sar_hip_copy_spans (16-byte non-temporal loads and stores, one
-    16-KiB piece per workgroup) at 1 GiB and 4 GiB, read + write bytes per second, HIP
-    events around 5 copies each.  The larger copy amortises the launch's head and tail
-    (round 1's microbenchmark: 6.12 / 6.34 TB/s at 1 / 4 GiB), so the fraction of copy
-    the bench reports is taken against the best copy it measured, not a flattering one."""
+    8-KiB piece per workgroup) of uniform random bytes (the headline's payload; constant
+    bytes copy faster) at 1 GiB and 4 GiB, read + write bytes per second, HIP events
+    around 5 copies each.  The larger copy amortises the launch's head and tail, so the
+    fraction of copy the bench reports is taken against the best copy it measured, not a
+    flattering one (tools/ubench_store.hip: the best plain copy form measured, 8-KiB
+    pieces with nt loads and stores, 6.06 / 6.21 TB/s at 1 / 4 GiB)."""
     best, per = 0.0, {}
     for nb in (1 << 30, 4 << 30):
         a = torch.empty(nb, dtype=torch.uint8, device=dev)
         b = torch.empty(nb, dtype=torch.uint8, device=dev)
-        a.fill_(7)
+        a.random_(0, 256)
         span = [(a.data_ptr(), b.data_ptr(), nb)]
         for _ in range(2):
             ctx.copy_spans(span)
@@ -408,11 +418,16 @@ def run_workload(args, env, headline: bool):
         return out
 
     plans = make_plans(args.batch_events)
+    groups = [seg.groups(p) for p in plans] if args.xcd_groups else None
     max_batch_pk = max(p.total_packets for p in plans)
     step_pk = sum(p.total_packets for p in plans)
     if args.reas in ("pipelined", "chained") and args.overlap:
         args.overlap = False                    # the pipeline is its own overlap
     nbuf = 2 if (args.overlap or args.reas == "pipelined") else 1
+    if args.lanes > 1:
+        if args.overlap or args.reas != "fused" or args.landing != "own":
+            raise SystemExit("--lanes runs the fused own-landing step")
+        nbuf = args.lanes
     if args.reas == "chained":
         args.chain_batches = max(1, min(8, args.chain_batches))
         nbuf = min(args.chain_batches, len(plans))
@@ -477,7 +492,9 @@ def run_workload(args, env, headline: bool):
 
     def reassemble(pk, ln, n, k, stream=None):
         """The receive side of one batch: one fused launch, or classify + scatter."""
-        if args.reas == "fused":
+        if args.reas == "fused" and groups is not None and groups[k][1]:
+            timed(fused_name, R.reassemble_groups, pk, stride, ln, n, groups[k][0], groups[k][1], stream=stream)
+        elif args.reas == "fused":
             timed(fused_name, R.reassemble, pk, stride, ln, n, stream=stream)
         else:
             w = works[k % nbuf]
@@ -566,9 +583,20 @@ def run_workload(args, env, headline: bool):
                 timed("segreas_kernel", seg.segment_reassemble_batches, chunk,
                       [bufs[(c0 + j) % nbuf] for j in range(len(chunk))], R)
             return
-        if not args.overlap:
-            pk, ln = bufs[0]
+        if args.lanes > 1 and not timing_on[0]:
+            for ls in lane_streams:
+                ls.wait_stream(s0)
             for k, p in enumerate(plans):
+                ls = lane_streams[k % args.lanes]
+                pk, ln = bufs[k % args.lanes]
+                seg.segment(p, pk, ln, stream=ls)
+                R.reassemble(pk, stride, ln, p.total_packets, stream=ls)
+            for ls in lane_streams:
+                s0.wait_stream(ls)
+            return
+        if not args.overlap:
+            for k, p in enumerate(plans):
+                pk, ln = bufs[k % nbuf] if args.lanes > 1 else bufs[0]
                 timed("seg_kernel", seg.segment, p, pk, ln)
                 reassemble(pk, ln, p.total_packets, k)
             return
@@ -590,6 +618,7 @@ def run_workload(args, env, headline: bool):
         s0.wait_stream(s1)
 
     side = torch.cuda.Stream() if args.overlap else None
+    lane_streams = [torch.cuda.Stream() for _ in range(args.lanes)] if args.lanes > 1 else []
 
     for _ in range(args.warmup):
         step()
@@ -873,6 +902,8 @@ def run_workload(args, env, headline: bool):
                            if spread and spread_graph[0] is not None else
                            "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times"),
                 "overlap": bool(args.overlap),
+                "lanes": args.lanes,
+                "xcd_groups": bool(groups and all(g[1] for g in groups)),
                 "reassembly": {"fused": ("reas_kernel per batch" if fused_name == "reas_kernel" else
                                          "reassemble_batch per batch, REFERENCE_ORDER: key pass, radix sort, "
                                          "per-key walk, scatter" if args.reference_order else
@@ -903,7 +934,7 @@ def run_workload(args, env, headline: bool):
                 "step_achieved_GBps": round(step_bytes * K / elapsed / 1e9, 1),
                 "copy_GBps": round(copy_gbps, 1) if copy_gbps else None,
                 "copy_what": ("best device-to-device copy on this GPU (e2sar_hip_copy_spans, 16-B non-temporal "
-                              "loads/stores) of 1 and 4 GiB, read + write bytes"),
+                              "loads/stores, 8-KiB pieces) of 1 and 4 GiB of random bytes, read + write bytes"),
                 "copy_GBps_by_size": copy_per,
                 "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
             },

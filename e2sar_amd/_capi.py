@@ -171,6 +171,8 @@ SIGNATURES = {
     "e2sar_hip_reas_destroy": (None, [vp]),
     "e2sar_hip_reas_arena": (vp, [vp]),
     "e2sar_hip_reassemble_batch": (i, [vp, vp, u32, vp, u32, u64, vp]),
+    "e2sar_hip_seg_groups": (i, [C.POINTER(SegEvent), u32, u32, u32, u32, C.POINTER(u32), u32, C.POINTER(u32)]),
+    "e2sar_hip_reassemble_groups": (i, [vp, vp, u32, vp, u32, vp, u32, u64, vp]),
     "e2sar_hip_reas_work_bytes": (sz, [u32]),
     "e2sar_hip_reas_classify": (i, [vp, vp, u32, vp, u32, u64, vp, sz, vp]),
     "e2sar_hip_reas_scatter": (i, [vp, vp, u32, u32, vp, sz, vp]),

@@ -631,6 +631,42 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     return E2SAR_HIP_OK;
 }
 
+int e2sar_hip_seg_groups(const e2sar_hip_seg_event *events, uint32_t nEvents, uint32_t maxPacketsPerEvent,
+                         uint32_t maxPldLen, uint32_t stride, uint32_t *starts, uint32_t cap, uint32_t *nGroups)
+{
+    if (!nGroups) return fail(E2SAR_HIP_ERR_PARAMETER, "nGroups is NULL");
+    *nGroups = 0;
+    if (nEvents && (!events || !starts)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL table");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
+    *nGroups = seg_groups(events, nEvents, maxPacketsPerEvent, maxPldLen, stride, starts, cap);
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reassemble_groups(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                                const uint32_t *d_lens, uint32_t nPackets, const uint32_t *d_starts,
+                                uint32_t nGroups, uint64_t now_ms, void *stream)
+{
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (nPackets == 0) return E2SAR_HIP_OK;
+    if (nGroups == 0 || !d_starts || ref_order(r) || (uint64_t)nPackets * stride > kFusedMaxBytes)
+        return e2sar_hip_reassemble_batch(r, d_packets, stride, d_lens, nPackets, now_ms, stream);
+    if (!d_packets || !d_lens) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    const uint32_t hl = r->cfg.withLBHeader ? E2SAR_HIP_LBRE_HDR_LEN : E2SAR_HIP_RE_HDR_LEN;
+    if ((stride & 15u) || stride < hl + 16u) return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and > header + 16");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    if ((uint64_t)nPackets * (stride >> 4) > 0xFFFFFFFFull) return fail(E2SAR_HIP_ERR_OUT_OF_RANGE, "batch too large");
+    if (nGroups > 0x7FFFFFFFu) return fail(E2SAR_HIP_ERR_PARAMETER, "too many groups");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
+    hipError_t e = launch_reassemble_groups(r->dev, d_packets, stride, d_lens, nPackets, d_starts, nGroups, now_ms, s);
+    if (e == hipSuccess) e = note_launch(r, s);
+    if (e != hipSuccess) return hip_fail(e, "reassembly launch (groups)");
+    return E2SAR_HIP_OK;
+}
+
 static int segreas(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches, uint32_t nBatches, int lbHdrVersion,
                    uint32_t maxPldLen, uint32_t stride, e2sar_hip_reas *r, uint64_t now_ms, void *stream)
 {

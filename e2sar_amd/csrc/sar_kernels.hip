@@ -122,13 +122,33 @@ __device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemp
 #endif
 __device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v)
 {
-#if E2SAR_REAS_NT_STORE
+#if E2SAR_REAS_NT_STORE == 2       // A/B: sc1 (write-through)
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#elif E2SAR_REAS_NT_STORE == 3     // A/B: sc1 nt
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#elif E2SAR_REAS_NT_STORE
     __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4_a4 *)(p));
 #else
     *(E2SAR_GLOBAL u32x4_a4 *)(p) = v;
 #endif
 }
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
+// Aligned 16-byte event store of the fused reassembly (A/B knob E2SAR_REAS_EV_STORE):
+// 0 nt (the line stays in the XCD's L2 until written back), 1 sc1 (write-through: the line
+// leaves L2, nothing of it is left dirty for the kernel-end write-back), 2 sc1 nt.
+#ifndef E2SAR_REAS_EV_STORE
+#define E2SAR_REAS_EV_STORE 0
+#endif
+__device__ __forceinline__ void st16_ev(uint8_t *p, u32x4 v)
+{
+#if E2SAR_REAS_EV_STORE == 1
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#elif E2SAR_REAS_EV_STORE == 2
+    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+#else
+    st16_nt(p, v);
+#endif
+}
 
 // Agent-coherent (sc1) forms for bytes handed from one workgroup to another inside a
 // launch (the chained segment -> reassemble form): the producer stores every handed-off
@@ -288,6 +308,9 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 #ifndef E2SAR_SEG_BLOCK
 #define E2SAR_SEG_BLOCK 256         // seg_kernel threads per workgroup (A/B knob)
 #endif
+#ifndef E2SAR_SEG_STORE
+#define E2SAR_SEG_STORE 0           // datagram stores: 0 plain, 1 sc1 (write-through), 2 nt (A/B knob)
+#endif
 // One round of a segmentation block: index-space chunks [j0, j0 + SB*U) of event ev,
 // bounded by jEnd (the event's chunk count, or the end of a local chained range).
 struct SegEv {
@@ -405,7 +428,8 @@ __device__ __forceinline__ void seg_round(const SegEv &E, uint8_t *__restrict__ 
         } else {
             o = u32x4{h.w0, h.w1, h.w2, h.w3};
         }
-        if (HO) st16_sc1(outR, 16u * (jj[u] - outJ0), o);
+        if (HO || E2SAR_SEG_STORE == 1) st16_sc1(outR, 16u * (jj[u] - outJ0), o);
+        else if (E2SAR_SEG_STORE == 2) st16_nt(out + 16u * jj[u], o);
         else st16(out + 16u * jj[u], o);
     }
 }
@@ -457,15 +481,30 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
 #endif
 }
 
+// stripe > 0 (XCD stripes): the dispatcher hands workgroup b to XCD b mod 8 (round robin,
+// checked by tools/ubench_l2keep.hip), and workgroup b = 8k + x takes unit
+// ((k / stripe) * 8 + x) * stripe + k % stripe, so units [m * stripe, (m + 1) * stripe) --
+// a stripe of consecutive datagrams -- are all written on XCD m mod 8.  A reassembly
+// launched with the matching group table (seg_groups) then reads every stripe on the XCD
+// that wrote it, which reads measurably faster than lines another XCD wrote, also from
+// the Infinity Cache.  Units are numbered e * blocksPerEvent + bx as
+// without stripes; units past nUnits exit.
 template <int U>
 __global__ __launch_bounds__(E2SAR_SEG_BLOCK) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                               uint32_t blocksPerEvent, int lbVersion,
                                                               uint32_t maxPld, uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t *__restrict__ lens,
-                                                              const uint32_t *__restrict__ dCount)
+                                                              const uint32_t *__restrict__ dCount, uint32_t stripe,
+                                                              uint32_t nUnits)
 {
+    uint32_t blk = blockIdx.x;
+    if (stripe) {
+        const uint32_t x = blk & 7u, k = blk >> 3;
+        blk = ((k / stripe) * 8u + x) * stripe + k % stripe;
+        if (blk >= nUnits) return;
+    }
     seg_block<U, false, E2SAR_SEG_BLOCK>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount,
-                                         blockIdx.x, 1u, nullptr);
+                                         blk, 1u, nullptr);
 }
 
 // ---------------------------------------------------------------------------------
@@ -1005,7 +1044,7 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
         (void)da_window(c, a, pi.hl, stride, sh);
         const u32x4 o = rot_down(x, sh >> 2);
         if (lo == 0u && hi == 16u) {
-            st16_nt(D, o);
+            st16_ev(D, o);
         } else {
 #pragma unroll
             for (uint32_t d = 0; d < 4; d++)
@@ -1168,13 +1207,21 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #endif
 }
 
+// starts (optional): group g is datagrams [starts[g], starts[g+1]) (<= 64), e.g. the XCD
+// stripes of the batch's segmentation (seg_groups); otherwise [g*G, g*G + G).
 template <int U, bool HO = false>
 __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
-                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr)
+                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr,
+                                           const uint32_t *__restrict__ starts = nullptr)
 {
-    const uint32_t g0 = g * G;
-    const uint32_t gn = (n - g0 < G) ? n - g0 : G;
+    uint32_t g0 = g * G;
+    uint32_t gn = (n - g0 < G) ? n - g0 : G;
+    if (starts) {
+        g0 = starts[g];
+        gn = starts[g + 1] - g0;
+        if (gn == 0u || gn > 64u) return;                            // empty stripe (host-checked <= 64)
+    }
     reas_range<U, HO>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
 }
 
@@ -1191,10 +1238,11 @@ template <int U>
 __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                            uint32_t stride, const uint32_t *__restrict__ lens,
                                                                            uint32_t n, uint64_t now, uint32_t G,
-                                                                           const GroupKeys *__restrict__ keys)
+                                                                           const GroupKeys *__restrict__ keys,
+                                                                           const uint32_t *__restrict__ starts)
 {
     __shared__ ReasGroupLds L;
-    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys);
+    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys, starts);
 }
 
 // Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
@@ -1406,6 +1454,63 @@ __device__ __forceinline__ void shift_store(const PktInfo pi, uint32_t c, u32x4 
     if (h4 < hi && h4 >= l4) store_bytes(D, o, h4, hi);
 }
 
+// E2SAR_SCATTER_SHIFT == 3 (A/B): the one-round group's source-aligned chunks go through
+// LDS.  Every dword of a payload is written to its destination phase in the group's LDS
+// copy of the slot (datagram p at p * (stride + 16), payload byte t at a + t, a = dst mod
+// 16), then after an LDS barrier every 16-byte event block is read back aligned and stored
+// aligned: the loads need nothing from the work records, the stores are whole aligned
+// 16-byte stores except at the payload's two edges.  A payload that is not dword-congruent
+// with its destination (never at dword-multiple maxPld) is stored from registers as before.
+template <int U>
+__device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x4 (&x)[U], const uint32_t (&pp)[U],
+                                                const uint32_t (&cc)[U], uint32_t nch, uint32_t gn, uint32_t stride)
+{
+    __shared__ uint32_t stage[(16384u + 64u * 16u) / 4u];
+    const uint32_t ps = stride + 16u;                                  // LDS bytes per datagram
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t i = (uint32_t)u * kBlock + threadIdx.x;
+        if (i >= nch) continue;
+        const PktInfo pi = sinfo[pp[u]];
+        if (pi.plen == 0u) continue;
+        const uint32_t a = (uint32_t)pi.dst & 15u;
+        if (((a - pi.hl) & 3u) != 0u) {                                // not dword-congruent
+            scatter_chunk(pi, cc[u], x[u]);
+            continue;
+        }
+        const uint32_t base = pp[u] * ps + a - pi.hl;                  // + slot byte offset
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++) {
+            const uint32_t s = 16u * cc[u] + 4u * d;
+            if (s >= pi.hl && s < pi.hl + pi.plen) stage[(base + s) >> 2] = x[u][d];
+        }
+    }
+    lds_barrier();
+    const uint32_t nbp = ps >> 4;                                      // 16-byte blocks per datagram
+    const uint32_t total = gn * nbp;
+    for (uint32_t k = threadIdx.x; k < total; k += kBlock) {
+        const uint32_t p = k / nbp, b = k - p * nbp;
+        const PktInfo pi = sinfo[p];
+        if (pi.plen == 0u) continue;
+        const uint32_t a = (uint32_t)pi.dst & 15u;
+        if (((a - pi.hl) & 3u) != 0u || 16u * b >= a + pi.plen) continue;
+        const uint32_t q = (p * ps + 16u * b) >> 2;
+        const u32x4 o{stage[q], stage[q + 1], stage[q + 2], stage[q + 3]};
+        uint8_t *D = reinterpret_cast<uint8_t *>((pi.dst & ~15ull) + 16ull * b);
+        const uint32_t lo = (b == 0u) ? a : 0u;
+        const uint32_t hi = (a + pi.plen - 16u * b < 16u) ? a + pi.plen - 16u * b : 16u;
+        if (lo == 0u && hi == 16u) {
+            st16_nt(D, o);
+            continue;
+        }
+#pragma unroll
+        for (uint32_t d = 0; d < 4; d++)
+            if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
+        const uint32_t t = hi & ~3u;                                   // sub-dword event tail
+        if (t < hi && t >= lo) store_bytes(D, o, t, hi);
+    }
+}
+
 // One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
 template <int U, bool NT>
 __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
@@ -1421,7 +1526,7 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     const PktInfo mine = ld_info(info + g0 + ((lane < gn) ? lane : 0u));
 
     const uint32_t spc = stride >> 4;
-    const uint32_t nch = gn * spc;
+    uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
     const bool last = (threadIdx.x & 63u) == 63u;
@@ -1462,6 +1567,12 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     }
     __syncthreads();
 
+#if E2SAR_SCATTER_SHIFT == 3
+    if (nch <= (uint32_t)(kBlock * U)) {
+        lds_stage_store<U>(sinfo, x, pp, cc, nch, gn, stride);
+        nch = 0;                                                     // done: skip the rounds below
+    }
+#endif
     for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
         if (r0) issue(r0);
 #pragma unroll
@@ -1781,10 +1892,13 @@ hipError_t launch_fill_bytes(void *p, int value, uint64_t n, hipStream_t stream)
 // Gather copy: blockIdx.y = span; 16-byte loads and stores when both ends are 16-byte
 // aligned (arena event buffers are 256-aligned; callers lay destinations out 64-aligned),
 // bytes otherwise and for the tail.
-// One workgroup copies one 16-KiB piece of one span (blockIdx.y): every thread issues its
-// four 16-byte non-temporal loads before any store, as seg_kernel does, so a large span
-// streams at the plain-copy rate (the bench's HBM calibration copies 1 GiB with it).
-constexpr uint32_t kCopyPiece = (uint32_t)kBlock * 16u * 4u;
+// One workgroup copies one 8-KiB piece of one span (blockIdx.y): every thread issues its
+// two 16-byte non-temporal loads before any store, as seg_kernel does, so a large span
+// streams at the plain-copy rate (the bench's HBM calibration copies 1 and 4 GiB with it).
+// 8-KiB pieces copy faster than 16-KiB ones on random bytes (tools/ubench_store.hip:
+// 6.06 vs 5.99 TB/s at 1 GiB, 6.21 vs 5.99 at 4 GiB).
+constexpr int kCopyU = 2;
+constexpr uint32_t kCopyPiece = (uint32_t)kBlock * 16u * kCopyU;
 __global__ __launch_bounds__(kBlock) void copy_spans_kernel(CopySpans cs)
 {
     if (blockIdx.y >= cs.n) return;
@@ -1797,14 +1911,14 @@ __global__ __launch_bounds__(kBlock) void copy_spans_kernel(CopySpans cs)
     uint64_t b0 = base;
     if (((sp.src | sp.dst) & 15u) == 0) {
         const uint64_t whole = sp.bytes & ~15ull;
-        u32x4 x[4];
+        u32x4 x[kCopyU];
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kCopyU; u++) {
             const uint64_t i = base + 16ull * ((uint64_t)u * kBlock + threadIdx.x);
             x[u] = (i + 16 <= whole) ? ld16_nt(src + i) : u32x4{0u, 0u, 0u, 0u};
         }
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
+        for (int u = 0; u < kCopyU; u++) {
             const uint64_t i = base + 16ull * ((uint64_t)u * kBlock + threadIdx.x);
             if (i + 16 <= whole) st16_nt(dst + i, x[u]);
         }
@@ -1954,25 +2068,107 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
 static_assert(E2SAR_SEG_U == 0 || E2SAR_SEG_U == 2 || E2SAR_SEG_U == 4, "seg_kernel is built for U = 2 or 4");
 static_assert(E2SAR_SCATTER_G <= 64 && E2SAR_SCATTER_LDS <= 65536 && E2SAR_PIPE_LDS <= 65536, "knob out of range");
 
+#ifndef E2SAR_SEG_STRIPE
+#define E2SAR_SEG_STRIPE 1          // seg_kernel writes XCD stripes (seg_groups); 0 = linear units (A/B knob)
+#endif
+
+template <int U>
+static uint32_t reas_resident_groups();
+
+// Geometry of seg_kernel for a batch: 16-byte chunks per thread, units per event and the
+// XCD stripe (units per stripe, 0 = none).  One place, so the reassembly group table of
+// seg_groups always matches the launch.
+struct SegGeom {
+    uint32_t U, unitChunks, bpe, stripe;
+    uint64_t nUnits;
+};
+static bool seg_geom(uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t stride, SegGeom &g)
+{
+    const uint32_t spc = stride >> 4;
+    const uint64_t chunks = (uint64_t)maxPacketsPerEvent * spc;
+    if (chunks > 0xFFFFFFFFull || spc == 0) return false;        // chunk index of an event is u32
+    g.U = E2SAR_SEG_U ? (uint32_t)E2SAR_SEG_U : (chunks <= (1u << 18) ? 2u : 4u);
+    g.unitChunks = (uint32_t)E2SAR_SEG_BLOCK * g.U;
+    g.bpe = cdiv(chunks, g.unitChunks);
+    g.nUnits = (uint64_t)g.bpe * nEvents;
+    // a stripe of about one fused reassembly group, min(49, 9216 / spc) datagrams, then
+    // balanced as reas_group_size balances its groups: the stripe count (= reassembly
+    // workgroups) just under a whole number of the chip's residency waves, if that keeps
+    // the stripe within [3/4, 4/3] of the target (205 x 1 MiB at MTU 1500: 8 -> 9 units,
+    // 3383 -> 3007 groups for 2 x 1536 resident)
+    g.stripe = 0;
+    if (!E2SAR_SEG_STRIPE) return true;
+    const uint32_t target = std::min<uint32_t>(49u, std::max<uint32_t>(1u, E2SAR_REAS_CHUNKS_PER_BLOCK / spc));
+    const uint32_t S0 = std::max<uint32_t>(1u, (uint32_t)((uint64_t)target * spc / g.unitChunks));
+    uint32_t best = S0;
+    const uint32_t cap = reas_resident_groups<E2SAR_REAS_U>();
+    if (cap && g.nUnits) {
+        const uint64_t waves = ((g.nUnits + S0 - 1) / S0 + cap - 1) / cap;
+        uint32_t bestDev = ~0u;
+        for (uint64_t k = (waves > 1 ? waves - 1 : waves); k <= waves; k++) {
+            const uint64_t c = (g.nUnits + k * cap - 1) / (k * cap);
+            if (c == 0 || c > 0xFFFFu || 4u * c < 3u * S0 || 3u * c > 4u * S0) continue;
+            const uint32_t dev = (uint32_t)(c > S0 ? c - S0 : S0 - c);
+            if (dev < bestDev) best = (uint32_t)c, bestDev = dev;
+        }
+    }
+    g.stripe = best;
+    return true;
+}
+
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           uint8_t *pkts, uint32_t stride, uint32_t *lens,
                           hipStream_t stream, const uint32_t *d_count)
 {
     if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
-    const uint64_t chunks = (uint64_t)maxPacketsPerEvent * (stride >> 4);
-    if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;   // chunk index of an event is u32
-    const uint32_t U = E2SAR_SEG_U ? (uint32_t)E2SAR_SEG_U : (chunks <= (1u << 18) ? 2u : 4u);
-    const uint32_t bpe = cdiv(chunks, (uint64_t)E2SAR_SEG_BLOCK * U);
-    const uint64_t grid = (uint64_t)bpe * nEvents;
+    SegGeom sg;
+    if (!seg_geom(nEvents, maxPacketsPerEvent, stride, sg)) return hipErrorInvalidValue;
+    const uint64_t grid = sg.stripe ? (sg.nUnits + 8ull * sg.stripe - 1) / (8ull * sg.stripe) * 8ull * sg.stripe
+                                    : sg.nUnits;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
-    if (U == 2)
-        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, bpe,
-                           lbVersion, maxPld, pkts, stride, lens, d_count);
+    if (sg.U == 2)
+        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, sg.bpe,
+                           lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
     else
-        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, bpe,
-                           lbVersion, maxPld, pkts, stride, lens, d_count);
+        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, sg.bpe,
+                           lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
     return hipGetLastError();
+}
+
+// Reassembly groups that match seg_kernel's XCD stripes for a planned batch (host event
+// table with pktBase, as e2sar_hip_seg_plan fills it): group m = the datagrams whose first
+// chunk lies in stripe m (units [m * stripe, (m + 1) * stripe)), written on XCD m mod 8;
+// reas_kernel workgroup m runs on the same XCD.  starts[0..nGroups], nGroups + 1 <= cap.
+// Returns nGroups, or 0 when the batch has no stripes or a group would exceed 64
+// datagrams (the caller then reassembles with the uniform groups).
+uint32_t seg_groups(const e2sar_hip_seg_event *ev, uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t maxPld,
+                    uint32_t stride, uint32_t *starts, uint32_t cap)
+{
+    SegGeom sg;
+    if (nEvents == 0 || maxPld == 0 || !seg_geom(nEvents, maxPacketsPerEvent, stride, sg) || !sg.stripe) return 0;
+    const uint64_t nGroups = (sg.nUnits + sg.stripe - 1) / sg.stripe;
+    if (nGroups + 1 > cap || nGroups > 0x7FFFFFFFull) return 0;
+    const uint32_t spc = stride >> 4;
+    uint64_t g = 0, total = 0;
+    starts[0] = 0;
+    for (uint32_t e = 0; e < nEvents; e++) {
+        const uint32_t np = (uint32_t)(((uint64_t)ev[e].bytes + maxPld - 1u) / maxPld);   // 0 for an empty event
+        const uint32_t base = ev[e].pktBase;
+        for (uint32_t q = 0; q < np; q++) {
+            const uint64_t m = ((uint64_t)e * sg.bpe + (uint64_t)q * spc / sg.unitChunks) / sg.stripe;
+            while (g < m) {
+                starts[++g] = base + q;
+                if (starts[g] - starts[g - 1] > 64u) return 0;
+            }
+        }
+        total = (uint64_t)base + np;
+    }
+    while (g < nGroups) {
+        starts[++g] = (uint32_t)total;
+        if (starts[g] - starts[g - 1] > 64u) return 0;
+    }
+    return (uint32_t)nGroups;
 }
 
 // ---------------------------------------------------------------------------------
@@ -2138,7 +2334,18 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
                            lens, n, now, G, groups, keys);
     }
     hipLaunchKernelGGL((reas_kernel<U>), dim3(groups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G,
-                       (const GroupKeys *)keys);
+                       (const GroupKeys *)keys, (const uint32_t *)nullptr);
+    return hipGetLastError();
+}
+
+hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                    uint32_t n, const uint32_t *starts, uint32_t nGroups, uint64_t now,
+                                    hipStream_t stream)
+{
+    constexpr int U = E2SAR_REAS_U;
+    if (n == 0 || nGroups == 0) return hipSuccess;
+    hipLaunchKernelGGL((reas_kernel<U>), dim3(nGroups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, 64u,
+                       (const GroupKeys *)nullptr, starts);
     return hipGetLastError();
 }
 

@@ -191,6 +191,12 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
                              const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream,
                              GroupKeys *keys = nullptr);
+// XCD-matched groups of a planned batch (seg_kernel's stripes) and the fused reassembly over them
+uint32_t seg_groups(const e2sar_hip_seg_event *ev, uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t maxPld,
+                    uint32_t stride, uint32_t *starts, uint32_t cap);
+hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
+                                    uint32_t n, const uint32_t *starts, uint32_t nGroups, uint64_t now,
+                                    hipStream_t stream);
 uint32_t reas_launch_groups(const ReasDev &R, uint32_t n, uint32_t stride);   // workgroups of reas_kernel
 // Chained form: segment each batch and reassemble the same datagrams, up to
 // kChainMaxBatches batches in one launch (segreas_kernel).  Batch b: nEvents descriptors at

@@ -135,6 +135,22 @@ class DeviceSegmenter:
         dev = torch.from_numpy(raw).to(self.ctx.torch_device, non_blocking=False)
         return SegPlan(arr, dev, n, int(tot.value), int(mx.value), aligned4)
 
+    def groups(self, plan: SegPlan):
+        """The reassembly groups that match this segmenter's XCD stripes for `plan`
+        (e2sar_hip_seg_groups): (device uint32 tensor of starts, nGroups), or (None, 0)
+        when the batch has no stripes.  For DeviceReassembler.reassemble_groups."""
+        spc = self.stride // 16
+        units = plan.n_events * max(1, (plan.max_packets_per_event * spc + 511) // 512)
+        cap = units + 2
+        starts = (C.c_uint32 * cap)()
+        ng = C.c_uint32()
+        check(lib().e2sar_hip_seg_groups(plan.host, plan.n_events, plan.max_packets_per_event, self.max_pld,
+                                         self.stride, starts, cap, C.byref(ng)))
+        if ng.value == 0:
+            return None, 0
+        host = np.frombuffer(bytes(starts), dtype=np.uint32)[: ng.value + 1].copy()
+        return torch.from_numpy(host.view(np.int32)).to(self.ctx.torch_device), int(ng.value)
+
     def alloc_packets(self, n_packets: int):
         pk = torch.empty(max(n_packets, 1) * self.stride, dtype=torch.uint8, device=self.ctx.torch_device)
         ln = torch.empty(max(n_packets, 1), dtype=torch.int32, device=self.ctx.torch_device)
@@ -242,6 +258,22 @@ class DeviceReassembler:
             raise ValueError("packet batch buffers too small")
         check(lib().e2sar_hip_reassemble_batch(
             self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
+            int(now_ms), C.c_void_p(_stream_handle(stream))))
+
+    def reassemble_groups(self, packets: torch.Tensor, stride: int, lens: torch.Tensor, n: int,
+                          starts: Optional[torch.Tensor], n_groups: int, now_ms: int = 0,
+                          stream: Optional[torch.cuda.Stream] = None) -> None:
+        """reassemble() over a group table (DeviceSegmenter.groups: the XCD stripes the batch
+        was segmented in), e2sar_hip_reassemble_groups."""
+        if n == 0:
+            return
+        if lens.numel() < n or packets.numel() < n * stride:
+            raise ValueError("packet batch buffers too small")
+        if starts is not None and starts.numel() < n_groups + 1:
+            raise ValueError("group table too small")
+        check(lib().e2sar_hip_reassemble_groups(
+            self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
+            C.c_void_p(starts.data_ptr() if starts is not None else 0), n_groups if starts is not None else 0,
             int(now_ms), C.c_void_p(_stream_handle(stream))))
 
     def relay_plan(self, events: torch.Tensor, counts: torch.Tensor, first_record: int, max_events: int,

@@ -257,6 +257,26 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
                                void *stream);
 
+/* Device-local round trips (a batch this library segmented is reassembled on the same GPU:
+ * loopback, relay, the device-resident benchmark).  e2sar_hip_segment_batch writes its
+ * datagrams in XCD stripes (runs of about one reassembly group of consecutive datagrams,
+ * all written on one of the eight XCDs); e2sar_hip_seg_groups returns, for the same planned
+ * host event table (pktBase filled by e2sar_hip_seg_plan), maxPacketsPerEvent, maxPldLen and
+ * stride, the reassembly groups that match them: group g = datagrams [starts[g],
+ * starts[g+1]) of the batch (at most 64), starts[0..*nGroups], *nGroups + 1 <= cap.
+ * *nGroups = 0 when the batch has no stripes (a group would exceed 64 datagrams).
+ * e2sar_hip_reassemble_groups is e2sar_hip_reassemble_batch with those groups (d_starts:
+ * the table copied to the device): workgroup g reassembles group g on the XCD that wrote
+ * it.  Results are those of e2sar_hip_reassemble_batch for any group table that covers
+ * [0, nPackets) in order; only the fused form takes groups (a batch above 320 MiB of slots,
+ * or reference-order mode, is reassembled as e2sar_hip_reassemble_batch does).  The
+ * datagrams' receive body is the same: e2sarDPReassembler.cpp:335-427. */
+int e2sar_hip_seg_groups(const e2sar_hip_seg_event *events, uint32_t nEvents, uint32_t maxPacketsPerEvent,
+                         uint32_t maxPldLen, uint32_t stride, uint32_t *starts, uint32_t cap, uint32_t *nGroups);
+int e2sar_hip_reassemble_groups(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
+                                const uint32_t *d_lens, uint32_t nPackets, const uint32_t *d_starts,
+                                uint32_t nGroups, uint64_t now_ms, void *stream);
+
 /* The same work as e2sar_hip_reassemble_batch split in two phases so a caller can
  * pipeline batches: classify (headers only: validate, look up / create, count) writes
  * per-datagram destinations into d_work; scatter moves the payload bytes and publishes

@@ -42,6 +42,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_U
 #define E2SAR_REAS_U 4
 #endif
+#ifndef E2SAR_SCATTER_U
+#define E2SAR_SCATTER_U E2SAR_REAS_U // 16-byte chunks per thread per round of the scatter forms
+#endif
 // seg_kernel's 16-byte output chunks per thread (U) is chosen per launch (launch_segment):
 // 8-KiB workgroups (U = 2) for events of up to 4 MiB of datagrams, 16-KiB (U = 4) above.
 // A/B (profiles/round2/ab2/segu*, suc3*, su9k): 205 x 1 MiB at MTU 1500, U = 2 1414-1422
@@ -2385,7 +2388,7 @@ hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t 
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
                                const void *work, hipStream_t stream, bool nt)
 {
-    constexpr int U = E2SAR_REAS_U;
+    constexpr int U = E2SAR_SCATTER_U;
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     const uint32_t G = scatter_group_size(stride);
@@ -2402,7 +2405,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
                                         uint64_t now, void *cwork, hipStream_t stream, bool nt)
 {
-    constexpr int U = E2SAR_REAS_U;
+    constexpr int U = E2SAR_SCATTER_U;
     if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream, nt);
     if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
     const uint8_t *sw = static_cast<const uint8_t *>(swork);

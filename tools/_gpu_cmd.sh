@@ -1,3 +1,7 @@
 set -e
-O=gpurun_out/perf_tool; mkdir -p $O
-for m in 9000 1500; do timeout -k 10 200 ./build/e2sar_perf --loopback -l 1048576 -n 2000 -m $m --rate -1 --port 10600 > $O/m$m.txt 2>&1 || { tail -20 $O/m$m.txt; exit 1; }; tail -6 $O/m$m.txt; done
+tools/ab_variants.sh r3s3_sc "--subs config3" base su8 su8g3 su5g2 g2
+cp gpurun_out/r3s3_sc/base.json gpurun_out/r3s3_sc/base1.json
+tools/ab_variants.sh r3s3_sc "--subs config3" base
+for f in gpurun_out/r3s3_sc/*.json; do python -c "
+import json,sys; d=json.loads(open('$f').read().strip().splitlines()[-1]); r=d['roofline']; c=d['reas_cold']; c3=d['config3']
+print('$f', d['value'], r['avg_launch_ms'], 'cold', c['value'], c['roofline']['all_launch_ms'], 'c3', c3['value'], c3['roofline']['avg_launch_ms'])"; done

@@ -975,6 +975,52 @@ __device__ __forceinline__ void classify_finish(const ReasDev &R, const Classifi
 // ---------------------------------------------------------------------------------
 // reassembly: one fused kernel
 
+// Dwords [lo/4, hi/4) of the register chunk v (lo < hi, both multiples of 4) to dst + lo:
+// a payload's first and last 16-byte chunk.  The store instructions a wave issues are what
+// its lanes need between them (exec-masked), so a wave holding one edge lane pays every
+// form the edge takes: E2SAR_EDGE_STORE 0 = one conditional dword store per dword (four
+// store instructions per edge wave, the round-2 form), 1 = one dwordx2 and/or one dword
+// store (two at most), 2 = one store of the edge's length (dword, dwordx2 or dwordx3).
+#ifndef E2SAR_EDGE_STORE
+#define E2SAR_EDGE_STORE 2
+#endif
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+typedef u32x2 __attribute__((aligned(4))) u32x2_a4;
+typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
+__device__ __forceinline__ void st8(uint8_t *p, uint32_t a, uint32_t b)
+{
+    *(E2SAR_GLOBAL u32x2_a4 *)(p) = u32x2{a, b};
+}
+__device__ __forceinline__ void st12(uint8_t *p, uint32_t a, uint32_t b, uint32_t c)
+{
+    // a 12-byte store (clang widens vec3 stores to 16 bytes, so no C++ form is safe here)
+    const u32x3 v{a, b, c};
+    // s_nop: the hazard recognizer does not see inside inline asm (a VALU write of the store's
+    // data registers right after a >64-bit store needs a wait state)
+    asm volatile("global_store_dwordx3 %0, %1, off\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void store_dwords(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
+{
+#if E2SAR_EDGE_STORE == 0
+#pragma unroll
+    for (uint32_t d = 0; d < 4; d++)
+        if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, v[d]);
+#else
+    const u32x4 w = rot_down(v, lo >> 2);
+    const uint32_t n = (hi - lo) >> 2;
+    uint8_t *p = dst + lo;
+#if E2SAR_EDGE_STORE == 1
+    if (n & 2u) st8(p, w.x, w.y);
+    if (n & 1u) st4(p + ((n & 2u) ? 8u : 0u), (n & 2u) ? w.z : w.x);
+#else
+    if (n == 3u) st12(p, w.x, w.y, w.z);
+    else if (n == 2u) st8(p, w.x, w.y);
+    else if (n == 1u) st4(p, w.x);
+    else st16u_nt(p, w);
+#endif
+#endif
+}
+
 __device__ __noinline__ void store_bytes(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
 {
     // bytes [lo, hi) of the 16-byte register chunk v to dst + (lo..hi); rare path
@@ -998,11 +1044,9 @@ __device__ __forceinline__ void scatter_chunk(const PktInfo pi, uint32_t c, u32x
     if (lo == 0 && hi == 16u && congruent) {
         st16u_nt(dst, v);
     } else if (congruent) {
-#pragma unroll
-        for (uint32_t d = 0; d < 4; d++)
-            if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, v[d]);
-        const uint32_t t = hi & ~3u;                               // sub-dword event tail
-        if (t < hi && t >= lo) store_bytes(dst, v, t, hi);
+        const uint32_t l4 = (lo + 3u) & ~3u, t = hi & ~3u;         // lo is a multiple of 4 here
+        if (l4 < t) store_dwords(dst, v, l4, t);
+        if (t < hi && t >= lo) store_bytes(dst, v, t, hi);         // sub-dword event tail
     } else {
         store_bytes(dst, v, lo, hi);
     }
@@ -1049,11 +1093,9 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
         if (lo == 0u && hi == 16u) {
             st16_ev(D, o);
         } else {
-#pragma unroll
-            for (uint32_t d = 0; d < 4; d++)
-                if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
-            const uint32_t t = hi & ~3u;                               // sub-dword event tail
-            if (t < hi && t >= lo) store_bytes(D, o, t, hi);
+            const uint32_t t = hi & ~3u;                               // lo = a is a multiple of 4
+            if (lo < t) store_dwords(D, o, lo, t);
+            if (t < hi && t >= lo) store_bytes(D, o, t, hi);           // sub-dword event tail
         }
     } else {
         const uint8_t *s = dgram + pi.hl + 16u * c - a;                // + lo >= hl

@@ -1651,6 +1651,78 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     }
 }
 
+// Chunk-range form of the scatter (G == 0 at launch, E2SAR_SCATTER_RANGE): workgroup blk
+// takes the batch's slot chunks [blk * K, blk * K + K), K = 256 * U, whatever datagrams
+// they belong to -- the loads are a plain linear copy of the slot buffer (pkts + 16 i), the
+// stores go to each chunk's datagram's destination.  At most kRangeSlots datagrams touch one
+// range (the host picks this form only for strides that guarantee it); a datagram's
+// completion is published by the range holding its first chunk.  Against groups of whole
+// datagrams, ranges keep every workgroup's load range 16-KiB and line-aligned: at MTU 9000 a
+// one-datagram group is 561 chunks, a workgroup boundary every 8976 bytes splits a line, and
+// in a microbenchmark the same copy ran 12 % slower (tools/ubench_dgram.hip: slotcopy_g1_u4
+// 202.7 vs lin16 176.6-184.3 us per 590 MB batch).  Measured in the scatter it did not pay
+// (config 3's 590 MB batch 224.7-234.9 vs 228.6-232.0 us; cold leg 2354 vs 2430 GiB/s,
+// profiles/round3/s3_range/), so it is an A/B build (E2SAR_SCATTER_RANGE=1), bit-exact on
+// the GPU suite.
+constexpr uint32_t kRangeSlots = 64;
+template <int U, bool NT>
+__device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                              uint32_t n, const PktInfo *__restrict__ info,
+                                              const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
+{
+    constexpr uint32_t K = (uint32_t)kBlock * U;
+    const uint32_t spc = stride >> 4;
+    const uint64_t total = (uint64_t)n * spc;
+    const uint64_t c0 = (uint64_t)blk * K;
+    const uint32_t nch = (total - c0 < K) ? (uint32_t)(total - c0) : K;
+    const uint32_t p0 = (uint32_t)(c0 / spc);
+    const uint32_t ns = (uint32_t)((c0 + nch - 1u) / spc) - p0 + 1u;   // <= kRangeSlots (host-checked)
+    const uint32_t skew = (uint32_t)(c0 - (uint64_t)p0 * spc);          // chunk of datagram p0 where we start
+    const uint32_t lane = threadIdx.x & 63u;
+    const PktInfo mine = ld_info(info + p0 + ((lane < ns) ? lane : 0u));
+
+    const float rspc = 1.0f / (float)spc;
+    const uint8_t *const base = pkts + 16ull * c0;
+    u32x4 x[U];
+    uint32_t pp[U], cc[U];
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
+        const uint32_t rc = (r < nch) ? r : 0u;
+        const uint32_t l = skew + rc;                                     // chunk index from datagram p0's start
+        uint32_t p = (uint32_t)((float)l * rspc);
+        if (p * spc > l) p--;
+        else if ((p + 1u) * spc <= l) p++;
+        pp[u] = p;
+        cc[u] = l - p * spc;
+        x[u] = NT ? ld16_nt(base + 16u * rc) : ld16(base + 16u * rc);
+    }
+    bool fins = false;
+    if (threadIdx.x < 64) {
+        const uint64_t lo = (uint64_t)R.arena, hi = lo + R.arenaBytes;
+        const bool inside = mine.plen == 0 || (mine.dst >= lo && mine.dst + mine.plen <= hi);
+        const bool own = lane < ns && (lane > 0u || skew == 0u);           // its first chunk is in this range
+        if (own && !inside) atomicOr(&R.ctl->errorFlags, 8u);
+        PktInfo v = (lane < ns && inside) ? mine : PktInfo{0ull, 0u, 0u};
+        fins = own && (v.hl & kPktCompletes) != 0u;
+        v.hl &= ~kPktCompletes;
+        sinfo[lane] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < U; u++) {
+        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
+        if (r >= nch) continue;
+        scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
+    }
+    if (fins) {
+        const FinishRec f = fin[p0 + lane];
+        const uint32_t fs = f.slot & ~kFinKeepSlot;
+        if (fs < R.tableSlots) complete_event(R, fs, f.ev, f.boff, f.bytes, f.d, f.frags, (f.slot & kFinKeepSlot) != 0u);
+        else atomicOr(&R.ctl->errorFlags, 8u);
+    }
+}
+
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,
                                                                uint32_t n, uint64_t now, PktInfo *__restrict__ info,
@@ -1666,7 +1738,8 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const u
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+    if (G == 0u) scatter_range<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
+    else scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
@@ -1685,7 +1758,8 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
                               blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
         return;
     }
-    scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+    if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+    else scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2292,6 +2366,26 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
 // that dependent table round trips see.
 
 
+#ifndef E2SAR_SCATTER_RANGE
+#define E2SAR_SCATTER_RANGE 0       // A/B: scatter workgroups over chunk ranges (1) instead of whole-datagram groups
+#endif
+// Scatter workgroups of the launch: chunk ranges of 256 * U chunks (scatter_range) when at
+// most kRangeSlots datagrams can touch one range, else groups of G whole datagrams.
+// Returns G (0 = ranges) and the workgroup count.
+static uint32_t scatter_group_size(uint32_t stride);
+static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
+{
+    constexpr uint32_t K = (uint32_t)kBlock * E2SAR_SCATTER_U;
+    const uint32_t spc = stride >> 4;
+    if (E2SAR_SCATTER_RANGE && !E2SAR_SCATTER_G && spc && (K + spc - 2u) / spc + 1u <= kRangeSlots) {
+        blocks = (uint32_t)(((uint64_t)n * spc + K - 1u) / K);
+        return 0u;
+    }
+    const uint32_t G = scatter_group_size(stride);
+    blocks = cdiv(n, G);
+    return G;
+}
+
 static uint32_t scatter_group_size(uint32_t stride)
 {
     // datagrams per scatter workgroup: at most E2SAR_SCATTER_CHUNKS_PER_BLOCK 16-byte chunks
@@ -2433,12 +2527,13 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     constexpr int U = E2SAR_SCATTER_U;
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
-    const uint32_t G = scatter_group_size(stride);
+    uint32_t blocks = 0;
+    const uint32_t G = scatter_geometry(stride, n, blocks);
     if (nt)
-        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
+        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
                            reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     else
-        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(cdiv(n, G)), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
+        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
                            reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
@@ -2452,15 +2547,16 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
     const uint8_t *sw = static_cast<const uint8_t *>(swork);
     uint8_t *cw = static_cast<uint8_t *>(cwork);
-    const uint32_t G = scatter_group_size(stride);
+    uint32_t sblocks = 0;
+    const uint32_t G = scatter_geometry(stride, sn, sblocks);
     const uint32_t nCls = cdiv(cn, kBlock);
     if (nt)
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
     else
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + cdiv(sn, G)), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
+    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                        reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);

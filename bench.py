@@ -35,6 +35,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
+BEST_COPY_GBS = 6240.0
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table: 8.0 TB/s spec
 XGMI_PEAK_GBS = 7 * 153.0  # per GPU, 7 xGMI links x ~153 GB/s (point to point)
 METRIC = "GiB/s event payload segmented+reassembled, device-resident, 1/2/4/8 MI355X"
@@ -937,6 +938,11 @@ def run_workload(args, env, headline: bool):
                               "loads/stores, 8-KiB pieces) of 1 and 4 GiB of random bytes, read + write bytes"),
                 "copy_GBps_by_size": copy_per,
                 "frac_of_copy": round(achieved / copy_gbps, 4) if copy_gbps else None,
+                # the best plain copy ever measured on MI355X in this repository (DESIGN 4.3:
+                # tools/ubench_copy.hip, aligned 16-B non-temporal copy of 1 GiB), so the
+                # fraction is never taken against a slower copy than the best one known
+                "best_copy_GBps": BEST_COPY_GBS,
+                "frac_of_best_copy": round(achieved / max(BEST_COPY_GBS, copy_gbps or 0.0), 4),
             },
             "xgmi": xgmi,
             "reas_cold": cold,

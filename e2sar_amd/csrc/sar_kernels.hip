@@ -1750,16 +1750,19 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
     const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
     const uint32_t *__restrict__ clens, uint32_t cn, uint64_t now, PktInfo *__restrict__ cinfo,
-    FinishRec *__restrict__ cfin, uint32_t nClsBlocks)
+    FinishRec *__restrict__ cfin, uint32_t nClsBlocks, uint32_t clsStart)
 {
     __shared__ PktInfo sinfo[64];
-    if (blockIdx.x < nClsBlocks) {
+    // workgroups [clsStart, clsStart + nClsBlocks) classify, the others scatter in order
+    const uint32_t b = blockIdx.x;
+    if (b - clsStart < nClsBlocks) {
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
-                              blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
+                              (b - clsStart) * (kBlock / 64) + (threadIdx.x >> 6));
         return;
     }
-    if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
-    else scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, blockIdx.x - nClsBlocks, sinfo);
+    const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
+    if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
+    else scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2366,6 +2369,10 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
 // that dependent table round trips see.
 
 
+#ifndef E2SAR_PIPE_CLS_AT
+#define E2SAR_PIPE_CLS_AT 75
+#endif
+static_assert(E2SAR_PIPE_CLS_AT >= 0 && E2SAR_PIPE_CLS_AT <= 100, "percent");
 #ifndef E2SAR_SCATTER_RANGE
 #define E2SAR_SCATTER_RANGE 0       // A/B: scatter workgroups over chunk ranges (1) instead of whole-datagram groups
 #endif
@@ -2550,16 +2557,23 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint32_t sblocks = 0;
     const uint32_t G = scatter_geometry(stride, sn, sblocks);
     const uint32_t nCls = cdiv(cn, kBlock);
+    // where the classify workgroups sit in the grid: E2SAR_PIPE_CLS_AT percent of the way
+    // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
+    // workgroup slots through their dependent round trips while the scatter ramps up; three
+    // quarters of the way in they run beside the scatter's last quarter and finish with it
+    // (cold leg, 205 x 1 MiB: 81.4-83.8 vs 83.9-87.0 us per launch over three boxes, 50 / 65 /
+    // 80 / 88 % in between; profiles/round3/s3_cls/)
+    const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * E2SAR_PIPE_CLS_AT / 100u);
     if (nt)
     hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
-                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
+                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls, clsStart);
     else
     hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
                        spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
                        reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
-                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls);
+                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls, clsStart);
     return hipGetLastError();
 }
 

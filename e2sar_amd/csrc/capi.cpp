@@ -224,11 +224,25 @@ int e2sar_hip_ctx_sync(e2sar_hip_ctx *ctx)
     return E2SAR_HIP_OK;
 }
 
+// A/B build knob: large device buffers (arena, e2sar_hip_device_alloc) physically contiguous
+// (hipDeviceMallocContiguous), falling back to hipMalloc when that fails
+#ifndef E2SAR_ALLOC_CONTIGUOUS
+#define E2SAR_ALLOC_CONTIGUOUS 0
+#endif
+static hipError_t dev_malloc(void **p, size_t bytes)
+{
+#if E2SAR_ALLOC_CONTIGUOUS
+    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
+    (void)hipGetLastError();
+#endif
+    return hipMalloc(p, bytes);
+}
+
 int e2sar_hip_device_alloc(e2sar_hip_ctx *ctx, size_t bytes, void **out)
 {
     if (!ctx || !out) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
     HIP_TRY(hipSetDevice(ctx->device));
-    hipError_t e = hipMalloc(out, bytes ? bytes : 1);
+    hipError_t e = dev_malloc(out, bytes ? bytes : 1);
     if (e != hipSuccess) return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc: ") + hipGetErrorString(e));
     return E2SAR_HIP_OK;
 }
@@ -490,7 +504,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
         reas_release(r);
         return fail(E2SAR_HIP_ERR_MEMORY, std::string("hipMalloc(state): ") + hipGetErrorString(e));
     }
-    e = hipMalloc(reinterpret_cast<void **>(&r->dev.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
+    e = dev_malloc(reinterpret_cast<void **>(&r->dev.arena), cfg->arenaBytes ? cfg->arenaBytes : 256);
     if (e != hipSuccess) {
         r->dev.arena = nullptr;
         reas_release(r);

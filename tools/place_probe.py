@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--copy", action="store_true",
                     help="also time a plain copy of the just-written datagram buffer (copy_spans, the floor)")
     ap.add_argument("--split", action="store_true", help="also time classify and scatter (streaming loads) apart")
+    ap.add_argument("--pk-lib", action="store_true",
+                    help="allocate the datagram buffer with e2sar_hip_device_alloc instead of torch")
     a = ap.parse_args()
     dev = torch.device("cuda", 0)
     ctx = sar.Context(0)
@@ -43,7 +45,15 @@ def main():
     n, stride = plan.total_packets, seg.stride
     offs = [int(float(x) * (1 << 20)) // 16 * 16 for x in a.offsets_mib.split(",")]
     shifts = [int(float(x) * (1 << 20)) for x in a.shifts_mib.split(",")]
-    pkall = torch.empty(n * stride + max(offs) + 16, dtype=torch.uint8, device=dev)
+    if a.pk_lib:
+        import ctypes as C
+        from e2sar_amd._capi import check, lib
+        nb = n * stride + max(offs) + 16
+        ptr = C.c_void_p()
+        check(lib().e2sar_hip_device_alloc(ctx.handle, C.c_size_t(nb), C.byref(ptr)))
+        pkall = sar._device_view(ptr.value, nb, dev)
+    else:
+        pkall = torch.empty(n * stride + max(offs) + 16, dtype=torch.uint8, device=dev)
     ln = torch.empty(n, dtype=torch.int32, device=dev)
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=4096, queue_capacity=4096,
                               arena_bytes=E * (B + 256) + max(shifts) + (64 << 20))

@@ -67,6 +67,8 @@ def parse(argv=None):
                     help="1: reassemble each batch over the group table that matches seg_kernel's XCD stripes "
                          "(e2sar_hip_seg_groups / e2sar_hip_reassemble_groups: every datagram read on the XCD "
                          "that wrote it)")
+    ap.add_argument("--guided", default="",
+                    help="A/B: 'F,SMIN,RESIDENT' guided group sizes for the fused reassembly (see run_workload)")
     ap.add_argument("--lanes", type=int, default=1,
                     help="independent segment -> reassemble pipelines on this many streams, batches dealt out "
                          "round-robin, each lane with its own datagram buffer (so the datagrams resident at "
@@ -420,6 +422,20 @@ def run_workload(args, env, headline: bool):
 
     plans = make_plans(args.batch_events)
     groups = [seg.groups(p) for p in plans] if args.xcd_groups else None
+    if args.guided:
+        # A/B: guided group sizes for the fused kernel (e2sar_hip_reassemble_groups with a
+        # host-built table): group k takes ceil(remaining / (F x resident)) datagrams, clamped
+        # to [SMIN, 64], so the groups dispatched last are the smallest and the launch's
+        # workgroups finish together
+        f, smin, resident = (float(x) for x in args.guided.split(","))
+        groups = []
+        for p in plans:
+            st, cur, n_ = [0], 0, p.total_packets
+            while cur < n_:
+                sz = int(min(64, max(smin, -(-(n_ - cur) // int(f * resident)))))
+                cur = min(n_, cur + sz)
+                st.append(cur)
+            groups.append((torch.tensor(st, dtype=torch.int32, device=dev), len(st) - 1))
     max_batch_pk = max(p.total_packets for p in plans)
     step_pk = sum(p.total_packets for p in plans)
     if args.reas in ("pipelined", "chained") and args.overlap:

@@ -1,3 +1,3 @@
 set -e
-A="--subs none --cold-steps 0 --cpu-seconds 0"
-tools/ab_args.sh r3s3_gs2 "g4|$A" "g20|$A --graph-steps 20" "g4|$A" "g20|$A --graph-steps 20" "g4|$A" "g20|$A --graph-steps 20" "g4|$A" "g20|$A --graph-steps 20"
+O=gpurun_out/r3s3_local; mkdir -p $O
+for m in 221 64 1024; do timeout -k 10 120 ./build/ubench_local $m 10 | tee -a $O/local.jsonl; done

@@ -26,9 +26,10 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ u32x4 ldnt(const uint8_t *p) { return __builtin_nontemporal_load((const G u32x4 *)p); }
 __device__ __forceinline__ void stnt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (G u32x4 *)p); }
-__device__ __forceinline__ u32x4 ldsc1(const uint8_t *p)
+// sc1 (L1-bypassing) 16-byte load through a buffer resource whose base is workgroup-uniform
+__device__ __forceinline__ u32x4 ldsc1(__amdgpu_buffer_rsrc_t r, uint32_t off)
 {
-    return __builtin_amdgcn_raw_buffer_load_b128(__builtin_amdgcn_make_buffer_rsrc(const_cast<uint8_t *>(p), (short)0, 0x7FFFFFFF, 0x00020000), 0, 0, 16);
+    return __builtin_amdgcn_raw_buffer_load_b128(r, (int)off, 0, 16);
 }
 
 template <int U>
@@ -68,11 +69,12 @@ __global__ __launch_bounds__(256) void local(const uint8_t *src, uint8_t *mid, u
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(mid + base, (short)0, 0x7FFFFFFF, 0x00020000);
     for (int r = 0; r < R; r++) {
         u32x4 v[U];
         // read back another thread's chunk (a rotation), so nothing comes from registers
 #pragma unroll
-        for (int u = 0; u < U; u++) v[u] = ldsc1(mid + base + r * RB + (u * 256 + ((threadIdx.x + 64) & 255)) * 16);
+        for (int u = 0; u < U; u++) v[u] = ldsc1(rs, (uint32_t)(r * RB + (u * 256 + ((threadIdx.x + 64) & 255)) * 16));
 #pragma unroll
         for (int u = 0; u < U; u++) stnt(dst + base + r * RB + (u * 256 + ((threadIdx.x + 64) & 255)) * 16, v[u]);
     }

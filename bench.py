@@ -427,14 +427,25 @@ def run_workload(args, env, headline: bool):
         # host-built table): group k takes ceil(remaining / (F x resident)) datagrams, clamped
         # to [SMIN, 64], so the groups dispatched last are the smallest and the launch's
         # workgroups finish together
-        f, smin, resident = (float(x) for x in args.guided.split(","))
+        # optional 4th/5th values LO,HI: the first RESIDENT groups take sizes spread over
+        # [LO, HI] (golden-ratio sequence), so the first residency wave does not finish -- and
+        # the second does not classify -- all at once
+        vals = [float(x) for x in args.guided.split(",")]
+        f, smin, resident = vals[:3]
+        lo_hi = vals[3:5] if len(vals) >= 5 else None
         groups = []
         for p in plans:
-            st, cur, n_ = [0], 0, p.total_packets
+            st, cur, n_, k = [0], 0, p.total_packets, 0
             while cur < n_:
-                sz = int(min(64, max(smin, -(-(n_ - cur) // int(f * resident)))))
+                if lo_hi and k < resident:
+                    fr = (k * 0.6180339887) % 1.0
+                    sz = int(round(lo_hi[0] + (lo_hi[1] - lo_hi[0]) * fr))
+                else:
+                    sz = -(-(n_ - cur) // int(f * resident))
+                sz = int(min(64, max(smin, sz)))
                 cur = min(n_, cur + sz)
                 st.append(cur)
+                k += 1
             groups.append((torch.tensor(st, dtype=torch.int32, device=dev), len(st) - 1))
     max_batch_pk = max(p.total_packets for p in plans)
     step_pk = sum(p.total_packets for p in plans)

@@ -54,7 +54,7 @@ struct e2sar_hip_reas {
     e2sar_hip_reas_config cfg{};
     ReasDev dev{};
     ReasDev alt{};                   // second slots + arena (COMPACTABLE), same ctl/lists
-    void *stateMem = nullptr;        // slots | ctl | shards | completed | lost
+    void *stateMem = nullptr;        // slots | ctl | shards | occupancy shards | completed | lost
     void *altSlots = nullptr;
     // Internal buffers, one set PER STREAM (two batches launched on different streams must
     // not share work records or ready counters while both run): the reference-order sort
@@ -494,7 +494,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->ctx = ctx;
     r->cfg = *cfg;
     const size_t slotsB = sizeof(ReasSlot) * (size_t)T;
-    const size_t ctlB = sizeof(ReasCtl) + sizeof(ReasShard) * kShards;
+    const size_t ctlB = sizeof(ReasCtl) + (sizeof(ReasShard) + sizeof(ReasOcc)) * kShards;
     const size_t compB = sizeof(e2sar_hip_event_rec) * (size_t)cfg->queueCapacity;
     const size_t lostB = sizeof(e2sar_hip_lost_rec) * (size_t)cfg->lostCapacity;
     const size_t total = slotsB + ctlB + compB + lostB;
@@ -904,14 +904,33 @@ static int wait_launches(e2sar_hip_reas *r)
     return E2SAR_HIP_OK;
 }
 
+// The control block with its occupancy counters live: ReasCtl's base plus the ReasOcc shards.
+static int read_ctl_occ(e2sar_hip_reas *r, ReasCtl &c)
+{
+    HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+    std::vector<ReasOcc> oc(kShards);
+    HIP_TRY(hipMemcpy(oc.data(), r->dev.shards + kShards, sizeof(ReasOcc) * kShards, hipMemcpyDeviceToHost));
+    long long used = c.tableUsed;
+    for (const auto &x : oc) {
+        c.inProgress += x.inProgress;
+        used += x.tableUsed;
+    }
+    c.tableUsed = (uint32_t)used;
+    return E2SAR_HIP_OK;
+}
+
 // Snapshot of the control block after every launch of this reassembler finished
 // (wait_launches), so the read-modify-write of the list counts in poll / lost_poll cannot
-// race a kernel's completion atomics.
+// race a kernel's completion atomics.  With `sum` (get_stats) the per-packet shards are
+// summed into it and the occupancy counters folded into c; poll / lost_poll need only the
+// list counts.
 static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
 {
     if (int rc = wait_launches(r)) return rc;
-    HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
-    if (sum) {
+    if (!sum) {
+        HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+    } else {
+        if (int rc = read_ctl_occ(r, c)) return rc;
         std::vector<ReasShard> sh(kShards);
         HIP_TRY(hipMemcpy(sh.data(), r->dev.shards, sizeof(ReasShard) * kShards, hipMemcpyDeviceToHost));
         *sum = ReasShard{};
@@ -920,6 +939,7 @@ static int read_ctl(e2sar_hip_reas *r, ReasCtl &c, ReasShard *sum = nullptr)
             sum->totalBytes += x.totalBytes;
             sum->badHeaderDiscards += x.badHeaderDiscards;
             sum->dataErrCnt += x.dataErrCnt;
+            sum->eventSuccess += x.eventSuccess;
         }
     }
     return E2SAR_HIP_OK;
@@ -987,7 +1007,7 @@ int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out)
     if (rc) return rc;
     out->enqueueLoss = c.enqueueLoss;
     out->reassemblyLoss = c.reassemblyLoss;
-    out->eventSuccess = c.eventSuccess;
+    out->eventSuccess = c.eventSuccess + t.eventSuccess;
     out->totalPackets = t.totalPackets;
     out->totalBytes = t.totalBytes;
     out->badHeaderDiscards = t.badHeaderDiscards;
@@ -1012,7 +1032,7 @@ int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream)
         ReasCtl c;
         if (int rc = wait_launches(r)) return rc;
         HIP_TRY(hipStreamSynchronize(s));
-        HIP_TRY(hipMemcpy(&c, r->dev.ctl, sizeof(ReasCtl), hipMemcpyDeviceToHost));
+        if (int rc = read_ctl_occ(r, c)) return rc;
         if (c.inProgress != 0) return fail(E2SAR_HIP_ERR_LOGIC, "events still in progress");
         if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
     }

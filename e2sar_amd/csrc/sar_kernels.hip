@@ -536,6 +536,16 @@ __device__ __forceinline__ void st_agent(T *p, typename id_t_<T>::type v)
 {
     __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+
+// occupancy shard of a table slot (ReasOcc follows the ReasShard array)
+__device__ __forceinline__ unsigned long long *occ_in_progress(const ReasDev &R, uint32_t slot)
+{
+    return reinterpret_cast<unsigned long long *>(&(reinterpret_cast<ReasOcc *>(R.shards + kShards) + slot % kShards)->inProgress);
+}
+__device__ __forceinline__ unsigned long long *occ_table_used(const ReasDev &R, uint32_t slot)
+{
+    return reinterpret_cast<unsigned long long *>(&(reinterpret_cast<ReasOcc *>(R.shards + kShards) + slot % kShards)->tableUsed);
+}
 // 16-byte agent-scope store and the pair of 16-byte agent-scope loads of records A and B
 // (the forms the compiler emits for 4/8-byte agent-scope atomics, at 16 bytes).  The
 // loads wait for their own results inside the asm.
@@ -614,7 +624,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             if (old == kEmpty && keyOnly) {
                 st16_agent(&sl->bufOff, u32x4{(uint32_t)kNoBuf, (uint32_t)(kNoBuf >> 32), 0u, kBNoItem});
                 st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
-                atomicAdd(&R.ctl->tableUsed, 1u);
+                atomicAdd(occ_table_used(R, h), 1ull);
                 res.slot = h;
                 active = false;
             } else if (old == kEmpty) {
@@ -628,8 +638,8 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 st_agent(&sl->created, now);
                 st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, 1u});
                 st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
-                atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), 1ull);
-                atomicAdd(&R.ctl->tableUsed, 1u);
+                atomicAdd(occ_in_progress(R, h), 1ull);
+                atomicAdd(occ_table_used(R, h), 1ull);
                 res.slot = h;
                 res.bytes = blen;
                 res.bufOff = boff;
@@ -924,8 +934,8 @@ __device__ void complete_event(const ReasDev &R, uint32_t slot, uint64_t ev, uin
 {
     ReasSlot *sl = R.slots + slot;
     if (!keepSlot) st_agent(&sl->state, (uint32_t)kDone);      // erase from the map (cpp:409)
-    atomicAdd(&R.ctl->eventSuccess, 1ull);                     // cpp:426
-    atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
+    atomicAdd(&R.shards[slot % kShards].eventSuccess, 1ull);   // cpp:426
+    atomicAdd(occ_in_progress(R, slot), ~0ull);
     bool lostOnEnqueue = (boff == kNoBuf);
     if (!lostOnEnqueue) {
         const uint32_t idx = atomicAdd(&R.ctl->nCompleted, 1u);
@@ -1971,7 +1981,7 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
         } else {
             sl->state = kDone;                                 // no item left under this key
         }
-        if (live) atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), (unsigned long long)live);
+        if (live) atomicAdd(occ_in_progress(R, slot), (unsigned long long)live);
         if (derr) atomicAdd(&R.shards[slot % kShards].dataErrCnt, (unsigned long long)derr);
     }
 }
@@ -2071,7 +2081,7 @@ __global__ __launch_bounds__(kBlock) void reas_gc_kernel(ReasDev R, uint64_t now
     if (now <= created || now - created <= timeout) return;     // inWaiting > timeout (cpp:262)
     if (atomicCAS(&sl->state, (uint32_t)kReady, (uint32_t)kLost) != kReady) return;
     atomicAdd(&R.ctl->reassemblyLoss, 1ull);
-    atomicAdd(reinterpret_cast<unsigned long long *>(&R.ctl->inProgress), ~0ull);
+    atomicAdd(occ_in_progress(R, s), ~0ull);
     const uint32_t li = atomicAdd(&R.ctl->nLost, 1u);
     if (li < R.lostCapacity) {
         e2sar_hip_lost_rec rec;
@@ -2096,6 +2106,10 @@ __global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dro
         R.ctl->tableUsed = 0;
         R.ctl->inProgress = 0;
         if (dropCompleted) R.ctl->nCompleted = 0;
+    }
+    if (s < kShards) {
+        *occ_in_progress(R, s) = 0ull;
+        *occ_table_used(R, s) = 0ull;
     }
 }
 
@@ -2152,6 +2166,7 @@ __global__ void reas_compact_finish(ReasDev to)
 {
     to.ctl->arenaTop = to.ctl->compactTop;
     to.ctl->tableUsed = to.ctl->compactUsed;
+    for (uint32_t k = 0; k < kShards; k++) *occ_table_used(to, k) = 0ull;
     to.ctl->compactTop = 0;
     to.ctl->compactUsed = 0;
 }

@@ -54,6 +54,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_DEFER_ACC
+#define E2SAR_REAS_DEFER_ACC 0       // reas_kernel: run tails of events of at least this many bytes
+#endif                              // add to the event accumulator after the copy (0: never)
 #ifndef E2SAR_CHAIN_SEG_U
 // chained form: seg blocks of 16 KiB (8-KiB blocks, as seg_kernel uses for 1 MiB events,
 // made the chained launch 147 -> 158 us: twice the blocks at the reassembly occupancy)
@@ -822,6 +825,9 @@ struct Classified {
 // carry the same (eventNum, dataId) form a run: only the run head touches the event
 // table and only the run tail adds to the event's byte/fragment counter, so the
 // per-event atomics are per run, not per datagram.
+// DeferAcc: the run tail's add to the event's accumulator is left to the caller (the fused
+// kernel issues it after its copy, so the copy's waits never sit behind that atomic).
+template <bool DeferAcc = false>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
                                     uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{})
 {
@@ -910,7 +916,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     out.rc = ic - hc;
     out.old = 0;
     out.tailAdd = tail && slot != kNoSlot;
-    if (out.tailAdd) {
+    if (out.tailAdd && !(DeferAcc && sbytes >= (uint32_t)E2SAR_REAS_DEFER_ACC)) {
         const uint64_t add = ((uint64_t)out.rc << kAccFragShift) | out.rb;
         out.old = atomicAdd(&R.slots[slot].acc, (unsigned long long)add);   // consumed in classify_finish
     }
@@ -1203,7 +1209,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 
     unsigned long long old = 0;
     if (w0) {
-        const Classified cl = classify_wave(R, raw, stride, lane < gn, now, g, key != nullptr, K);
+        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(R, raw, stride, lane < gn, now, g, key != nullptr, K);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -1244,6 +1250,12 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 
     if (w0 && L.tail[lane]) {
         Classified cl;
+#if E2SAR_REAS_DEFER_ACC
+        // in-order vmcnt: issued before the copy, this atomic's return (slow when ~100 groups
+        // of one event add at once) would gate wave 0's first copy wait
+        if (L.bytes[lane] >= (uint32_t)E2SAR_REAS_DEFER_ACC)
+            old = atomicAdd(&R.slots[L.slot[lane]].acc, ((unsigned long long)L.rc[lane] << kAccFragShift) | L.rb[lane]);
+#endif
         cl.old = old;
         cl.ev = L.ev[lane];
         cl.boff = L.boff[lane];

@@ -55,8 +55,8 @@ constexpr int kBlock = 256;
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
 #ifndef E2SAR_REAS_DEFER_ACC
-#define E2SAR_REAS_DEFER_ACC 0       // reas_kernel: run tails of events of at least this many bytes
-#endif                              // add to the event accumulator after the copy (0: never)
+#define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
+#endif                               // add to the event accumulator after the copy (0: never)
 #ifndef E2SAR_CHAIN_SEG_U
 // chained form: seg blocks of 16 KiB (8-KiB blocks, as seg_kernel uses for 1 MiB events,
 // made the chained launch 147 -> 158 us: twice the blocks at the reassembly occupancy)

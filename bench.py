@@ -151,11 +151,13 @@ def host_cpu_info() -> dict:
 def cpu_baseline(args, budget_s: float):
     """The oracle (plain-C restatement of _send + recv body) on the host cores, on a bounded
     sample of the same workload: each thread segments + reassembles the sample's events
-    (64 x 1 MiB by default) repeatedly.  Timed on 1 thread and on T threads, budget_s each; the
-    T-thread rate is the reported baseline.  T = the CPUs this process may use, capped at
-    16: the GPU box allots 16 host CPUs per GPU (OMP_NUM_THREADS=16 there) although nproc
-    shows the whole machine.  ctypes releases the GIL around every C call."""
-    import threading
+    (64 x 1 MiB by default) repeatedly, budget_s per thread count.  Three thread counts:
+    1; T = the GPU's share of the host (the CPUs this process may use, capped at 16: the
+    GPU box allots 16 host CPUs per GPU, OMP_NUM_THREADS=16 there) -- the reported `value`;
+    and every CPU this process may use (`all_cores`, sched_getaffinity = nproc on the box),
+    SURVEY 8(d)'s nproc figure.  The threads are POSIX threads inside the oracle library
+    (oracle/cpu_bench.c), so no interpreter lock sits between them."""
+    import ctypes as C
 
     import numpy as np
 
@@ -170,52 +172,24 @@ def cpu_baseline(args, budget_s: float):
     # one (tools/cpu_baseline_sweep.sh)
     n_ev = int(os.environ.get("E2SAR_CPU_EVENTS", 0)) or max(1, min(64, (64 << 20) // B))
     mp = O.max_pld_len(args.mtu)
-    stride = (36 + mp + 15) // 16 * 16
-    npk = O.num_packets(B, mp)
-    events = [S.event_bytes(i, B) for i in range(n_ev)]
-
-    import ctypes as C
-
-    def worker(deadline, out, idx):
-        L = O.lib()
-        pk = np.zeros((npk, stride), np.uint8)
-        ln = np.zeros(npk, np.uint32)
-        evp = C.POINTER(C.c_uint8)()
-        nb, en, di = C.c_size_t(), C.c_uint64(), C.c_uint16()
-        done = 0
-        while True:
-            r = O.Reassembler(True, 1 << 20)
-            for i, ev in enumerate(events):
-                L.e2o_segment_event(ev.ctypes.data, B, i, S.DATA_ID, S.entropy(i), S.lb_tick(i),
-                                    args.lb_version, mp, pk.ctypes.data, stride, ln.ctypes.data)
-                r.push_batch(pk, ln)
-                # getEvent hands the event buffer over and the caller frees it
-                # (e2sarDPReassembler.cpp:626-641; delete[] in bin/e2sar_perf.cpp:299)
-                assert L.e2o_reas_pop(r.h, C.byref(evp), C.byref(nb), C.byref(en), C.byref(di)) == 0
-                assert nb.value == B
-                L.e2o_free(evp)
-            done += n_ev * B
-            del r
-            if time.perf_counter() >= deadline:
-                break
-        out[idx] = done
+    sample = np.concatenate([S.event_bytes(i, B) for i in range(n_ev)])
+    L = O.lib()
 
     def run(threads):
-        out = [0] * threads
-        t0 = time.perf_counter()
-        ts = [threading.Thread(target=worker, args=(t0 + budget_s, out, k)) for k in range(threads)]
-        for t in ts:
-            t.start()
-        for t in ts:
-            t.join()
-        dt = time.perf_counter() - t0
-        return sum(out) / dt / 2**30, sum(out) // (n_ev * B), dt
+        done, dt = C.c_uint64(), C.c_double()
+        rc = L.e2o_cpu_bench(sample.ctypes.data, n_ev, B, args.lb_version, mp, S.DATA_ID, threads,
+                             budget_s, C.byref(done), C.byref(dt))
+        if rc != 0:
+            raise RuntimeError(f"oracle CPU baseline failed on {threads} threads")
+        return done.value / dt.value / 2**30, done.value // (n_ev * B), dt.value
 
     info = host_cpu_info()
     omp = int(os.environ.get("OMP_NUM_THREADS", info["allowed"]))
     T = max(1, min(16, omp, info["allowed"]))
     v1, p1, d1 = run(1)
     vT, pT, dT = run(T) if T > 1 else (v1, p1, d1)
+    A = info["allowed"]
+    vA, pA, dA = run(A) if A > T else (vT, pT, dT)
     what = (f"MTU {args.mtu}: oracle segment_event (header + payload memcpy per datagram) then recv "
             f"body (parse, map lookup, memcpy) into a fresh event handed out like getEvent and freed, "
             f"each thread {n_ev} x {B} B events per pass")
@@ -224,6 +198,9 @@ def cpu_baseline(args, budget_s: float):
             "host": {**info, "threads_used": T,
                      "cap": "min(16, OMP_NUM_THREADS, sched_getaffinity): the GPU box's CPU share per GPU"},
             "single_core": {"value": round(v1, 4), "cores": 1, "sample": f"{p1} passes in {d1:.1f} s"},
+            "all_cores": {"value": round(vA, 4), "cores": A, "sample": f"{pA} passes on {A} threads in {dA:.1f} s",
+                          "note": "every CPU sched_getaffinity allows this process (the whole host on the GPU box, "
+                                  "shared with the other GPUs' jobs)"},
             "config1_loopback": cpu_loopback(args, min(5.0, budget_s))}
 
 

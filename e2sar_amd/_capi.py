@@ -190,6 +190,7 @@ SIGNATURES = {
     "e2sar_hip_route_append": (i, [vp, vp, u32, vp, u32, i, u32, u32, i, vp, vp, u32, vp, vp, sz, vp]),
     "e2sar_hip_reas_set_owner": (i, [vp, u32, u32]),
     "e2sar_hip_reas_set_cold": (i, [vp, i]),
+    "e2sar_hip_reas_forget_stream": (i, [vp, vp]),
 }
 
 

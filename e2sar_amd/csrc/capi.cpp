@@ -157,6 +157,20 @@ static void free_internal(e2sar_hip_reas *r)
     r->streams.clear();
 }
 
+// Free the internal buffers of stream s (caller holds r->mu and knows none of its launches
+// still runs).  Buffers a graph capture may hold are retired instead, as in grow().
+static void drop_scratch(e2sar_hip_reas *r, hipStream_t s)
+{
+    auto it = r->scratch.find(s);
+    if (it == r->scratch.end()) return;
+    for (void *p : {it->second.roScratch, it->second.roWork, it->second.tiles, it->second.keys}) {
+        if (!p) continue;
+        if (r->sawCapture) r->retired.push_back(p);
+        else (void)hipFree(p);
+    }
+    r->scratch.erase(it);
+}
+
 // Free whatever a partly built reassembler holds (every pointer starts null).
 static void reas_release(e2sar_hip_reas *r)
 {
@@ -563,7 +577,9 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
 {
     if (!r) return;
     (void)hipSetDevice(r->ctx->device);
-    (void)hipStreamSynchronize(r->ctx->stream);
+    // launches on any stream (the caller's, a graph replay's) may still use the table, the
+    // arena and the internal buffers: wait for the device before the first hipFree
+    (void)hipDeviceSynchronize();
     if (r->alt.slots) {
         // the two tables/arenas may have been swapped: free whichever is not in stateMem
         auto *base = static_cast<uint8_t *>(r->stateMem);
@@ -573,7 +589,6 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     }
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
-    (void)hipDeviceSynchronize();          // launches on other streams may still use the internal buffers
     free_internal(r);
     delete r;
 }
@@ -893,14 +908,21 @@ static int wait_launches(e2sar_hip_reas *r)
     for (auto it = r->streams.begin(); it != r->streams.end();) {
         const hipError_t e = hipEventRecord(r->waitEv, *it);
         if (e == hipErrorInvalidHandle || e == hipErrorContextIsDestroyed || e == hipErrorInvalidResourceHandle) {
+            // a stream destroyed without e2sar_hip_reas_forget_stream: its work finished when
+            // it was destroyed; its scratch goes with it
             (void)hipGetLastError();
-            it = r->streams.erase(it);                 // destroyed stream: nothing left to wait for
+            drop_scratch(r, *it);
+            it = r->streams.erase(it);
             continue;
         }
         if (e != hipSuccess) return hip_fail(e, "hipEventRecord");
         HIP_TRY(hipEventSynchronize(r->waitEv));
         ++it;
     }
+    // every launch of this reassembler has finished and none was captured, so no kernel and
+    // no graph can still hold a buffer that an earlier growth retired
+    for (void *p : r->retired) (void)hipFree(p);
+    r->retired.clear();
     return E2SAR_HIP_OK;
 }
 
@@ -1158,6 +1180,18 @@ int e2sar_hip_reas_set_owner(e2sar_hip_reas *r, uint32_t world, uint32_t self)
     std::lock_guard<std::mutex> lk(r->mu);
     r->dev.ownWorld = r->alt.ownWorld = world;
     r->dev.ownSelf = r->alt.ownSelf = self;
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_reas_forget_stream(e2sar_hip_reas *r, void *stream)
+{
+    if (!r || !stream) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL argument");
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(r->ctx->device));
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    HIP_TRY(hipStreamSynchronize(s));
+    r->streams.erase(s);
+    drop_scratch(r, s);
     return E2SAR_HIP_OK;
 }
 

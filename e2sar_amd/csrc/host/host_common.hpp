@@ -33,6 +33,10 @@ inline uint64_t now_us()
 // does not change under it) -- the reference measures it in every Segmenter constructor
 float clock_entropy_bits();
 
+// Segmenter MTU rules (segmenter.cpp): interface/override resolution and the 9000-byte limit
+uint32_t resolve_mtu(uint16_t flagsMtu, uint32_t ifMtu, const std::string &iface);
+void check_mtu_limit(uint32_t mtu);
+
 inline uint64_t steady_ms()
 {
     return (uint64_t)std::chrono::duration_cast<std::chrono::milliseconds>(

@@ -136,6 +136,29 @@ Segmenter::Impl::~Impl()
     if (stream) e2sar_hip_stream_destroy(stream);
 }
 
+namespace detail {
+// e2sarDPSegmenter.cpp:56-110: mtu 0 takes the outgoing interface's MTU as reported; an
+// override must not exceed it (an interface that reports 0 accepts any override)
+uint32_t resolve_mtu(uint16_t flagsMtu, uint32_t ifMtu, const std::string &iface)
+{
+    if (flagsMtu == 0) {
+        if (ifMtu == 0) throw E2SARException("Outgoing interface MTU is reported as 0, please use manual override of MTU size");
+        return ifMtu;
+    }
+    if (ifMtu > 0 && flagsMtu > ifMtu)
+        throw E2SARException("Segmenter flags MTU override value exceeds outgoing interface MTU of " + iface);
+    return flagsMtu;
+}
+
+// e2sarDPSegmenter.hpp:307-308, applied to the resolved MTU: an auto-detected 9216 (jumbo
+// Ethernet) or 65520 (IPoIB) is refused like an override above 9000, so the datagram slots
+// never outgrow the 9000-byte layout the data plane is sized for
+void check_mtu_limit(uint32_t mtu)
+{
+    if (mtu > 9000) throw E2SARException("MTU set too long, limit 9000");
+}
+}  // namespace detail
+
 // e2sarDPSegmenter.hpp:298-317 + ctor checks at cpp:52-53
 void Segmenter::Impl::sanity()
 {
@@ -144,7 +167,7 @@ void Segmenter::Impl::sanity()
     if (flags.numSendSockets > 128) throw E2SARException("Too many sending sockets threads requested, limit 128");
     if (flags.numSendSockets == 0) throw E2SARException("At least one sending socket is required");
     if (flags.syncPeriodMs > 10000) throw E2SARException("Sync period too long, limit 10s");
-    if (flags.mtu > 9000) throw E2SARException("MTU set too long, limit 9000");
+    detail::check_mtu_limit(mtu);          // the resolved MTU, as the reference checks it (hpp:307)
     if (flags.useCP && !uri.has_syncAddr()) throw E2SARException("Sync address not present in the URI");
     if (!uri.has_dataAddr()) throw E2SARException("Data address is not present in the URI");
     if (mtu <= e2sar_hip_total_hdr_len(useV6 ? 1 : 0))
@@ -157,9 +180,9 @@ static void init_impl(Segmenter::Impl &m)
     if (!m.uri.has_dataAddrv4() && m.uri.has_dataAddrv6()) m.useV6 = true;
     // outgoing interface and its MTU for the URI's data address (e2sarDPSegmenter.cpp:56-110),
     // with the reference's rules: a failed lookup throws whatever the override; mtu 0 takes
-    // the interface's MTU as reported (loopback's 65536 then fails the 9000-byte sanity
-    // check below, as in the reference, hpp:307-308); an override must not exceed the
-    // interface's MTU (an interface that reports 0 accepts any override).
+    // the interface's MTU as reported (loopback's 65536 reads as 0 through the reference's
+    // u_int16_t, e2sarNetUtil.cpp:147-149, and is refused; a jumbo 9216 fails the 9000-byte
+    // check in sanity(), hpp:307-308); an override must not exceed the interface's MTU.
     auto addr = m.useV6 ? m.uri.get_dataAddrv6() : m.uri.get_dataAddrv4();
     if (addr.has_error()) throw E2SARException("Data address is not present in the URI");
     auto intf = NetUtil::getInterfaceAndMTU(addr.value().first);
@@ -167,15 +190,7 @@ static void init_impl(Segmenter::Impl &m)
         throw E2SARException("Unable to determine outgoing interface for LB destination address " +
                              addr.value().first + ": " + intf.error().message());
     m.iface = std::get<0>(intf.value());
-    const uint32_t ifMtu = std::get<1>(intf.value());
-    if (m.flags.mtu == 0) {
-        if (ifMtu == 0) throw E2SARException("Outgoing interface MTU is reported as 0, please use manual override of MTU size");
-        m.mtu = ifMtu;
-    } else {
-        if (ifMtu > 0 && m.flags.mtu > ifMtu)
-            throw E2SARException("Segmenter flags MTU override value exceeds outgoing interface MTU of " + m.iface);
-        m.mtu = m.flags.mtu;
-    }
+    m.mtu = detail::resolve_mtu(m.flags.mtu, std::get<1>(intf.value()), m.iface);
     m.sanity();
     m.maxPld = e2sar_hip_max_pld_len(m.mtu, m.useV6 ? 1 : 0);     // cpp:113
     m.addEntropy = !(detail::clock_entropy_bits() > kMinClockEntropy);   // cpp:50

@@ -451,6 +451,14 @@ int e2sar_hip_reas_set_owner(e2sar_hip_reas *r, uint32_t world, uint32_t self);
  * reassembled where they landed, then datagrams received from other ranks) tells each
  * launch how to load them. */
 int e2sar_hip_reas_set_cold(e2sar_hip_reas *r, int cold);
+/* Before destroying a stream that launched through this reassembler: wait for the stream's
+ * work, stop tracking it and free its internal buffers (or retire them, if a launch of this
+ * reassembler was ever captured).  Snapshots (poll, lost_poll, get_stats) wait for every
+ * stream the reassembler launched on, so a stream must outlive the reassembler's last
+ * snapshot unless it is forgotten first: HIP may hand a destroyed stream's handle to a new
+ * stream.  (A snapshot that finds a handle already invalid drops it the same way.)  No
+ * reference counterpart: the reference's receive threads own their sockets for their life. */
+int e2sar_hip_reas_forget_stream(e2sar_hip_reas *r, void *stream);
 
 #ifdef __cplusplus
 }

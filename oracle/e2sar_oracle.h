@@ -99,6 +99,12 @@ size_t e2o_segment_batch(const uint8_t *events, size_t n, size_t bytes,
                          int lbHdrVersion, size_t maxPldLen,
                          uint8_t *pkts, size_t stride, uint32_t *lens);
 
+/* ---- CPU baseline timing (cpu_bench.c; bench.py's cpu_baseline leg only) ----
+ * `threads` POSIX threads each segment + reassemble the nEvents-event sample until
+ * `seconds` have passed; returns 0 with the payload bytes done and the wall time. */
+int e2o_cpu_bench(const uint8_t *events, size_t nEvents, size_t bytes, int lbHdrVersion, size_t maxPldLen,
+                  uint16_t dataId, int threads, double seconds, uint64_t *bytesDone, double *elapsed);
+
 #ifdef __cplusplus
 }
 #endif

@@ -72,6 +72,9 @@ def lib() -> C.CDLL:
                                         C.POINTER(C.c_uint64)]
         L.e2o_reas_get_stats.restype = None
         L.e2o_reas_get_stats.argtypes = [vp, C.POINTER(Stats)]
+        L.e2o_cpu_bench.restype = C.c_int
+        L.e2o_cpu_bench.argtypes = [u8p, sz, sz, C.c_int, sz, C.c_uint16, C.c_int, C.c_double,
+                                    C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
         _lib = L
     return _lib
 

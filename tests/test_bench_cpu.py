@@ -23,6 +23,8 @@ def test_cpu_baseline_reports_the_contract_fields(monkeypatch):
     assert r["unit"] == "GiB/s" and r["kind"] == "port" and r["value"] > 0
     assert 1 <= r["cores"] <= 2 and r["single_core"]["cores"] == 1 and r["single_core"]["value"] > 0
     assert "MTU 1500" in r["sample"]
+    a = r["all_cores"]
+    assert a["cores"] == bench.host_cpu_info()["allowed"] and a["value"] > 0
 
 
 def test_gpus_n_starts_one_rank_per_gpu(monkeypatch):

@@ -632,9 +632,16 @@ def test_random_workload_segment_then_reassemble(hip, seed):
     mtu = rnd.choice([80, 104, 576, 1499, 1500, 4000, 9000])
     ver = rnd.choice([2, 3])
     cap = 150_000 if mtu >= 1499 else 20_000
+    # every fourth seed at MTU >= 1499 draws events up to 8 MiB, so the fused kernel's
+    # deferred run-tail add (events >= E2SAR_REAS_DEFER_ACC = 4 MiB) meets random workloads
+    big = seed % 4 == 3 and mtu >= 1499
+    if big:
+        cap = 8 << 20
     evs, keys = [], set()
-    while len(evs) < rnd.randint(1, 12):
+    while len(evs) < (rnd.randint(1, 4) if big else rnd.randint(1, 12)):
         size = rnd.choice([1, 3, 4, 17, 1435, 1436, 1437]) if rnd.random() < 0.3 else rnd.randint(1, cap)
+        if big and len(evs) == 0:
+            size = rnd.randint(4 << 20, 8 << 20)
         e, d = rnd.randint(0, (1 << 40) - 1), rnd.choice([1, 2, 4321])
         if (e, d) in keys:
             continue
@@ -659,3 +666,68 @@ def test_random_workload_segment_then_reassemble(hip, seed):
     got, st, _ = _reas_gpu(hip, pk, ln, True, batches=rnd.randint(1, 4), mode=mode)
     _check_reas(got, st, ref, rst)
     assert len(got) == len(evs) and st.errorFlags == 0
+
+
+def _singleton_at(order_len, batches, group, pos):
+    """True when datagram `pos` of a stream of order_len, cut into `batches` linspace batches
+    of fused groups of `group`, is the last datagram of its group (its run cannot extend
+    past it)."""
+    cuts = np.linspace(0, order_len, batches + 1).astype(int)
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        if a <= pos < b:
+            return (pos - a + 1) % group == 0 or pos + 1 == b
+    return False
+
+
+@pytest.mark.parametrize("mtu", [1500, 9000])
+@pytest.mark.parametrize("batches,group", [(1, 49), (3, 64), (1, 7), (2, 16)])
+def test_reas_large_events_with_loss_fused(hip, mtu, batches, group):
+    # events of 4-8 MiB through the fused reas_kernel, where run tails of events of at
+    # least 4 MiB add to the accumulator after the copy (E2SAR_REAS_DEFER_ACC,
+    # sar_kernels.hip reas_range): A loses one datagram to a bad RE version (never
+    # completes, GC reports it lost), B receives one full datagram twice, in its middle
+    # (curBytes passes its length without meeting it, so it never completes -- the
+    # reference's rule, cpp:398-403), C arrives with its tail shuffled, D intact.  Events,
+    # bytes, every counter and the lost records equal the oracle's
+    # (e2sarDPReassembler.cpp:331-427).
+    # The device adds per run, in any order: B could meet its length only if its last add
+    # were a run of exactly one full datagram, which needs B's first datagram alone in its
+    # group; A's tail is trimmed until the cuts do not isolate it (asserted below).
+    sizes = [4 << 20, (6 << 20) + 13, (8 << 20) - 5, 8 << 20]
+    evs, pk, ln = _events_stream(4, sizes, mtu, seed=70 + mtu)
+    mp = O.max_pld_len(mtu)
+    per = [O.num_packets(z, mp) for z in sizes]
+    assert (sizes[1] - (per[1] - 1) * mp) != mp               # B's tail is short
+    st = np.cumsum([0] + per)
+    pk, ln = pk.copy(), ln.copy()
+    pk[st[0] + per[0] // 2, 16] = 0x20                           # A: RE version 2 -> invalid
+    rnd = random.Random(mtu)
+    c_idx = list(range(st[2], st[3]))
+    tail = c_idx[1:]
+    rnd.shuffle(tail)                                            # C: offset 0 first, tail shuffled
+    b_idx = list(range(st[1], st[2]))
+    dup = b_idx[len(b_idx) // 3]                                 # B: one full datagram twice
+    b_order = b_idx[: len(b_idx) // 2] + [dup] + b_idx[len(b_idx) // 2:]
+    a_n = per[0]
+    while True:
+        order = list(range(st[0], st[0] + a_n)) + b_order + [c_idx[0]] + tail + list(range(st[3], st[4]))
+        if not _singleton_at(len(order), batches, group, a_n):
+            break
+        a_n -= 1
+    assert a_n > per[0] // 2 + 1                                 # A keeps its bad datagram
+    pk, ln = pk[order], ln[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    assert set(ref) == {(2, 4321), (3, 4321)}
+    got, stt, R = _reas_gpu(hip, pk, ln, True, batches=batches, now=100, arena=64 << 20,
+                            mode="fused", group_size=group)
+    _check_reas(got, stt, ref, rst)
+    assert stt.badHeaderDiscards == 1 and stt.errorFlags == 0
+    assert got[(2, 4321)][0] == evs[2].tobytes() and got[(3, 4321)][0] == evs[3].tobytes()
+    ro = O.Reassembler(True)
+    ro.set_time(100)
+    ro.push_batch(pk, ln)
+    ro.pop_all()
+    ro.set_time(1000)
+    ro.gc(500)
+    R.gc(now_ms=1000, timeout_ms=500)
+    assert sorted((r.eventNum, r.dataId, r.numFragments) for r in R.lost_poll()) == sorted(ro.lost_pop_all())

@@ -17,11 +17,19 @@ $(LIBDIR)/libe2sar_hip.so: $(HIP_SRCS) $(HIP_HDRS)
 oracle:
 	$(MAKE) -C oracle
 
+# A/B-only launch forms (include/e2sar_hip_experimental.h) in a library of their own;
+# run with E2SAR_HIP_LIB=build/variants/lib_experimental.so
+experimental: build/variants/lib_experimental.so
+
+build/variants/lib_experimental.so: $(HIP_SRCS) $(HIP_HDRS) include/e2sar_hip_experimental.h
+	@mkdir -p build/variants
+	$(HIPCC) $(HIPFLAGS) -DE2SAR_HIP_EXPERIMENTAL=1 $(INC) -shared -o $@ $(HIP_SRCS)
+
 clean:
 	rm -rf $(LIBDIR) e2sar_amd/csrc/*.o
 	$(MAKE) -C oracle clean
 
-.PHONY: all oracle clean
+.PHONY: all oracle clean experimental
 
 # ---- reference-shaped C++ facade (pure C++ over the C ABI) ----
 CXX ?= g++

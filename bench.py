@@ -86,8 +86,6 @@ def parse(argv=None):
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
-    ap.add_argument("--spread-eager", action="store_true",
-                    help="spread landing: launch the landing part eagerly too (default: one HIP graph per step)")
     ap.add_argument("--table-factor", type=int, default=8,
                     help="event-table slots = next power of two >= factor x events per step")
     ap.add_argument("--cold-steps", type=int, default=10,
@@ -100,10 +98,12 @@ def parse(argv=None):
     ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="pipelined",
                     help="launch form of the cold leg (split: classify + scatter launches, timed apart; "
                          "pipelined: classify(0), then scatter(b) beside classify(b+1) in one launch)")
-    ap.add_argument("--subs", default="mtu9000,config3",
-                    help="sub-legs reported beside the headline at N=1 (comma list of mtu9000, config3; "
-                         "'none' to skip): north_star's MTU 9000 half (1 MiB events) and BASELINE config 3 "
-                         "(8 MiB events at MTU 9000, 70 events = 65,730 datagrams per launch)")
+    ap.add_argument("--subs", default="auto",
+                    help="sub-legs reported beside the headline (comma list of mtu9000, config3, spread; "
+                         "'none' to skip; 'auto' = mtu9000,config3 at N=1 and spread at N>1): north_star's "
+                         "MTU 9000 half (1 MiB events), BASELINE config 3 (8 MiB events at MTU 9000, 70 "
+                         "events = 65,730 datagrams per launch) and BASELINE config 4 (datagrams landing "
+                         "spread over the ranks, exchanged over RCCL)")
     ap.add_argument("--quiet", action="store_true")
     return ap.parse_args(argv)
 
@@ -320,7 +320,7 @@ def main():
 
     # the other half of north_star's target and BASELINE config 3, in the same run: each a
     # workload of its own (fresh buffers), its own roofline; `value` above stays config 2's
-    subs = [s for s in args.subs.split(",") if s and s != "none"] if world == 1 and args.landing == "own" else []
+    subs = sub_legs(args, world)
     for name in subs:
         over = SUB_LEGS[name]
         a = argparse.Namespace(**{**vars(args), **over, "cold_steps": 0, "cpu_seconds": 0.0})
@@ -333,6 +333,9 @@ def main():
                 "ms_per_step": sl["ms_per_step"], "steps": sl["steps"], "verified": sl["config"]["verified_roundtrip"],
                 "reassembly": sl["config"]["reassembly"], "launch": sl["config"]["launch"],
                 "roofline": sl["roofline"], "leg_seconds": round(time.perf_counter() - t0, 1)}
+            if name == "spread":
+                line[name].update({"parallelism": sl["config"]["parallelism"], "xgmi": sl["xgmi"],
+                                   "exchange": sl["spread"]})
 
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
@@ -340,6 +343,17 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def sub_legs(args, world: int):
+    """The sub-legs of this run: --subs, where 'auto' is north_star's MTU 9000 half and
+    BASELINE config 3 at N=1, and config 4 (spread landing) at N>1.  Only beside an
+    own-landing headline."""
+    if args.landing != "own":
+        return []
+    if args.subs == "auto":
+        return ["mtu9000", "config3"] if world == 1 else ["spread"]
+    return [s for s in args.subs.split(",") if s and s != "none"]
 
 
 class Env:
@@ -352,6 +366,7 @@ class Env:
 SUB_LEGS = {
     "mtu9000": {"mtu": 9000},
     "config3": {"mtu": 9000, "event_bytes": 8 << 20, "events": 280, "batch_events": 70},
+    "spread": {"landing": "spread"},
 }
 
 
@@ -450,22 +465,20 @@ def run_workload(args, env, headline: bool):
 
     spread = args.landing == "spread"
     if spread:
-        # each batch lands in one reused buffer (as the own-landing leg's); while it is still
-        # in the Infinity Cache the datagrams this rank owns are reassembled where they
-        # landed (the reassembler is set to this rank's ownership) and the FOREIGN ones are
-        # appended to per-owner regions (e2sar_hip_route_append); at the end of the step one
-        # all-to-all-v sends the regions (split sizes from one all-gather of the counters:
-        # one host read per step) and the received datagrams -- cold by then -- are
-        # reassembled in the pipelined form with streaming loads
-        from e2sar_amd.dist import RegionRouter
+        # BASELINE config 4, per landed batch (e2sar_amd.dist.SpreadPipeline): each batch lands
+        # in one reused buffer (as the own-landing leg's); while it is still in the Infinity
+        # Cache the datagrams this rank owns are reassembled where they landed (the
+        # reassembler is set to this rank's ownership) and the FOREIGN ones are appended to
+        # per-owner regions (e2sar_hip_route_append); then batch b's counts are all-gathered
+        # and its regions exchanged (RCCL all-to-all over xGMI) on a communication stream and
+        # what arrived is reassembled (classify + scatter, streaming loads) on a third stream,
+        # while batch b+1 lands: the step costs max(landing, exchange), not their sum
+        from e2sar_amd.dist import SpreadPipeline
         land = seg.alloc_packets(max_batch_pk)
-        router = RegionRouter(ctx, stride, step_pk, max_batch_pk, world, rank)
-        recv_cap = 2 * step_pk + 1024
-        recv_bufs = (torch.empty(recv_cap * stride, dtype=torch.uint8, device=dev),
-                     torch.empty(recv_cap, dtype=torch.int32, device=dev))
-        recv_work = [R.alloc_work(max_batch_pk) for _ in range(2)]
+        pipe = SpreadPipeline(ctx, R, stride, max_batch_pk, world, rank)
+        R.set_cold(True)                   # received datagrams: streaming loads in the scatter
         if args.overlap or not args.eager or args.reas != "fused":
-            log(args, "landing=spread: the exchange reads its split sizes on the host -> eager, fused, no overlap")
+            log(args, "landing=spread: per-batch exchange reads split sizes on the host -> eager, fused, no overlap")
         args.overlap = False
         args.reas = "fused"
         args.eager = True
@@ -490,6 +503,21 @@ def run_workload(args, env, headline: bool):
         timing.append((name, e0, e1))
         return r
 
+    def timed_on(name, stream, fn, *a, **kw):
+        """timed() for a launch on an explicit stream (the spread pipeline's three streams)."""
+        if not timing_on[0]:
+            return fn(*a, stream=stream, **kw)
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        r = fn(*a, stream=stream, **kw)
+        e1.record(stream)
+        timing.append((name, e0, e1))
+        return r
+
+    if spread:
+        pipe.timed = timed_on
+
     # reassemble_batch runs classify + scatter inside for batches above 320 MiB of slots
     # (e2sar_hip.h); the timing entry then covers both launches
     fused_name = ("reassemble_batch_ro" if args.reference_order else
@@ -506,55 +534,17 @@ def run_workload(args, env, headline: bool):
             timed("reas_classify_kernel", R.classify, pk, stride, ln, n, w, stream=stream)
             timed("reas_scatter_kernel", R.scatter, pk, stride, n, w, stream=stream)
 
-    last_counts = []
-    last_recv = [0]
-
-    def spread_landed():
-        """The device part of a spread-landing step (capturable): every batch lands, this
-        rank's events are reassembled in place (hot), the foreign datagrams appended to the
-        per-owner regions."""
+    def step_spread():
+        """Datagrams land on this rank whatever their owner (SpreadPipeline): this rank's
+        events are reassembled in place (hot), the foreign ones routed per batch, exchanged
+        (RCCL all-to-all) and reassembled by their owners while the next batch lands."""
         lpk, lln = land
         R.recycle(force=True)
-        router.reset()
+        pipe.begin_step()
         for p in plans:
             timed("seg_kernel", seg.segment, p, lpk, lln)
-            timed("reas_kernel", R.reassemble, lpk, stride, lln, p.total_packets)
-            timed("route_kernels", router.route, lpk, lln, p.total_packets)
-
-    spread_graph = [None]
-
-    def step_spread():
-        """Datagrams land on this rank whatever their owner: this rank's events are
-        reassembled in place (hot), the foreign ones routed, exchanged (RCCL all-to-all-v)
-        and reassembled by their owners.  The landing part replays as a HIP graph once
-        captured (not in the per-kernel timing pass); the exchange needs a host read of the
-        split sizes, so it and the received datagrams' reassembly run eagerly."""
-        if spread_graph[0] is not None and not timing_on[0]:
-            spread_graph[0].replay()
-        else:
-            spread_landed()
-        if world > 1:
-            rpk, rln, n = timed("exchange", router.exchange, out=recv_bufs)
-            last_counts[:] = [int(c) for c in router.running.tolist()]
-        else:
-            last_counts[:] = [int(c) for c in router.running.tolist()]   # the step's one host read (nothing is foreign)
-            if last_counts[0]:
-                raise SystemExit("spread landing at N=1 routed a datagram away")
-            rpk, rln, n = recv_bufs[0], recv_bufs[1], 0
-        last_recv[0] = n
-        if n:
-            R.set_cold(True)
-            spans = [(c0, min(n, c0 + max_batch_pk)) for c0 in range(0, n, max_batch_pk)]
-            a0, b0 = spans[0]
-            timed("reas_classify_kernel", R.classify, rpk[a0 * stride:], stride, rln[a0:], b0 - a0, recv_work[0])
-            for k, (a, b) in enumerate(spans):
-                if k + 1 < len(spans):
-                    c, d = spans[k + 1]
-                    timed("reas_scatter_classify_kernel", R.scatter_classify, stride, rpk[a * stride:], b - a,
-                          recv_work[k % 2], rpk[c * stride:], rln[c:], d - c, recv_work[(k + 1) % 2])
-                else:
-                    timed("reas_scatter_kernel", R.scatter, rpk[a * stride:], stride, b - a, recv_work[k % 2])
-            R.set_cold(False)
+            pipe.land(lpk, lln, p.total_packets)
+        pipe.flush()
 
     def step():
         """One step: recycle the event table/arena, then segment -> reassemble every batch.
@@ -700,12 +690,6 @@ def run_workload(args, env, headline: bool):
         graph = capture(step, G)
         if not args.no_verify:
             verified = verify() and verified is not False
-    elif spread and not args.spread_eager:
-        spread_graph[0] = capture(spread_landed, 1)
-        step()
-        torch.cuda.synchronize()
-        if not args.no_verify:
-            verified = verify_spread() and verified is not False
 
     def run_timed(fn, g, k):
         """k steps (k/G graph replays, or k eager steps) between barriers; max over ranks."""
@@ -788,11 +772,16 @@ def run_workload(args, env, headline: bool):
     # spread landing: the exchange's bytes against the xGMI links: this rank's
     # datagram slots + lengths sent to other ranks per step / the exchange's time
     xgmi = None
-    if spread and world > 1 and "exchange" in avg and avg["exchange"] > 0:
-        sent = sum(c for j, c in enumerate(last_counts) if j != rank) * (stride + 4)
-        xgmi = {"bytes_sent_per_step": sent, "exchange_ms": round(avg["exchange"], 5),
-                "achieved": round(sent / (avg["exchange"] * 1e-3) / 1e9, 1), "peak": XGMI_PEAK_GBS,
-                "unit": "GB/s", "frac": round(sent / (avg["exchange"] * 1e-3) / 1e9 / XGMI_PEAK_GBS, 4),
+    if spread and world > 1 and "exchange" in per and sum(per["exchange"]) > 0:
+        # per step: this rank's foreign datagram slots + lengths sent / the exchanges' time
+        # (the step's all-to-alls, each timed on the communication stream; they overlap the
+        # landing of the next batch, so their sum is not a share of the step)
+        sent = pipe.sent * (stride + 4)
+        ex_ms = sum(per["exchange"]) / max(1, args.roofline_steps)
+        xgmi = {"bytes_sent_per_step": sent, "exchange_ms_per_step": round(ex_ms, 5),
+                "exchanges_per_step": len(per["exchange"]) // max(1, args.roofline_steps),
+                "achieved": round(sent / (ex_ms * 1e-3) / 1e9, 1), "peak": XGMI_PEAK_GBS,
+                "unit": "GB/s", "frac": round(sent / (ex_ms * 1e-3) / 1e9 / XGMI_PEAK_GBS, 4),
                 "backend": backend}
 
     total_payload = E * B * world * K
@@ -902,9 +891,8 @@ def run_workload(args, env, headline: bool):
                 "parallelism": (f"eventNum % {world} sharding (no collective)" if not spread else
                                 f"eventNum % {world} owners, datagrams land spread: route + all-to-all-v "
                                 f"({backend}) + reassemble"),
-                "launch": ("landing part (segment, in-place reassembly, route) as one hipGraph per step; "
-                           "count read, exchange and received-datagram reassembly eager"
-                           if spread and spread_graph[0] is not None else
+                "launch": ("eager, three streams: landing (segment, in-place reassembly, route) | count "
+                           "all-gather + all-to-all | reassembly of what arrived" if spread and world > 1 else
                            "eager" if args.eager else f"hipGraph of {G} step(s), replayed {K // G} times"),
                 "overlap": bool(args.overlap),
                 "lanes": args.lanes,
@@ -952,10 +940,12 @@ def run_workload(args, env, headline: bool):
             "reas_cold": cold,
         }
         if spread:
-            line["spread"] = {"foreign_sent_per_step": sum(c for j, c in enumerate(last_counts) if j != rank),
-                              "received_per_step": last_recv[0], "route": "foreign only (e2sar_hip_route_foreign)",
+            line["spread"] = {"foreign_sent_per_step": pipe.sent, "received_per_step": pipe.received,
+                              "route": "foreign only, per batch (e2sar_hip_route_append into per-owner regions)",
                               "in_place": "reas_kernel with e2sar_hip_reas_set_owner(world, rank)",
-                              "received_form": "reas_classify + reas_scatter_classify (pipelined, cold loads)"}
+                              "exchange": "per batch: count all-gather + all_to_all on a communication stream, "
+                                          "overlapping the next batch's landing (dist.SpreadPipeline)",
+                              "received_form": "reas_classify + reas_scatter (streaming loads) on a third stream"}
     # free this workload's device buffers before the next one (sub-legs)
     R.close()
     return line

@@ -164,15 +164,11 @@ SIGNATURES = {
     "e2sar_hip_seg_plan": (i, [C.POINTER(SegEvent), u32, sz, C.POINTER(u32), C.POINTER(u32)]),
     "e2sar_hip_segment_batch": (i, [vp, vp, u32, u32, i, u32, i, vp, u32, vp, vp]),
     "e2sar_hip_segment_batch_dev": (i, [vp, vp, vp, u32, u32, i, u32, vp, u32, vp, vp]),
-    "e2sar_hip_segment_reassemble_batch": (i, [vp, vp, u32, u32, u32, i, u32, vp, u32, vp, vp, u64, vp]),
-    "e2sar_hip_segment_reassemble_batches": (i, [vp, vp, u32, i, u32, u32, vp, u64, vp]),
     "e2sar_hip_relay_plan": (i, [vp, u32, u32, sz, u64, C.c_uint16, vp, vp, vp]),
     "e2sar_hip_reas_create": (i, [vp, C.POINTER(ReasConfig), C.POINTER(vp)]),
     "e2sar_hip_reas_destroy": (None, [vp]),
     "e2sar_hip_reas_arena": (vp, [vp]),
     "e2sar_hip_reassemble_batch": (i, [vp, vp, u32, vp, u32, u64, vp]),
-    "e2sar_hip_seg_groups": (i, [C.POINTER(SegEvent), u32, u32, u32, u32, C.POINTER(u32), u32, C.POINTER(u32)]),
-    "e2sar_hip_reassemble_groups": (i, [vp, vp, u32, vp, u32, vp, u32, u64, vp]),
     "e2sar_hip_reas_work_bytes": (sz, [u32]),
     "e2sar_hip_reas_classify": (i, [vp, vp, u32, vp, u32, u64, vp, sz, vp]),
     "e2sar_hip_reas_scatter": (i, [vp, vp, u32, u32, vp, sz, vp]),
@@ -191,6 +187,15 @@ SIGNATURES = {
     "e2sar_hip_reas_set_owner": (i, [vp, u32, u32]),
     "e2sar_hip_reas_set_cold": (i, [vp, i]),
     "e2sar_hip_reas_forget_stream": (i, [vp, vp]),
+}
+
+# include/e2sar_hip_experimental.h: A/B-only launch forms, bound when the loaded library
+# was built with them (`make experimental`, E2SAR_HIP_LIB=build/variants/lib_experimental.so)
+EXPERIMENTAL_SIGNATURES = {
+    "e2sar_hip_segment_reassemble_batch": (i, [vp, vp, u32, u32, u32, i, u32, vp, u32, vp, vp, u64, vp]),
+    "e2sar_hip_segment_reassemble_batches": (i, [vp, vp, u32, i, u32, u32, vp, u64, vp]),
+    "e2sar_hip_seg_groups": (i, [C.POINTER(SegEvent), u32, u32, u32, u32, C.POINTER(u32), u32, C.POINTER(u32)]),
+    "e2sar_hip_reassemble_groups": (i, [vp, vp, u32, vp, u32, vp, u32, u64, vp]),
 }
 
 
@@ -219,8 +224,26 @@ def lib() -> C.CDLL:
             fn = getattr(L, name)
             fn.restype = res
             fn.argtypes = args
+        for name, (res, args) in EXPERIMENTAL_SIGNATURES.items():
+            if hasattr(L, name):
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
         _lib = L
     return _lib
+
+
+def has_experimental() -> bool:
+    """True when the loaded library carries the A/B-only forms of e2sar_hip_experimental.h."""
+    L = lib()
+    return all(hasattr(L, n) for n in EXPERIMENTAL_SIGNATURES)
+
+
+def need_experimental(what: str) -> None:
+    if not has_experimental():
+        raise E2SARHipError(ERR_LOGIC, f"{what} is an A/B-only form (include/e2sar_hip_experimental.h): build it "
+                                       "with `make experimental` and load E2SAR_HIP_LIB=build/variants/"
+                                       "lib_experimental.so")
 
 
 def check(rc: int) -> int:

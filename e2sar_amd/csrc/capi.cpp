@@ -4,6 +4,12 @@
 // device allocation of the reassembly state, and the hand-off of device records to
 // the caller.  Every byte of event or datagram data is moved by the kernels in
 // sar_kernels.hip; there is no CPU fallback.
+#ifndef E2SAR_HIP_EXPERIMENTAL
+#define E2SAR_HIP_EXPERIMENTAL 0
+#endif
+#if E2SAR_HIP_EXPERIMENTAL
+#include "e2sar_hip_experimental.h"
+#endif
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -660,6 +666,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
     return E2SAR_HIP_OK;
 }
 
+#if E2SAR_HIP_EXPERIMENTAL
 int e2sar_hip_seg_groups(const e2sar_hip_seg_event *events, uint32_t nEvents, uint32_t maxPacketsPerEvent,
                          uint32_t maxPldLen, uint32_t stride, uint32_t *starts, uint32_t cap, uint32_t *nGroups)
 {
@@ -761,6 +768,8 @@ int e2sar_hip_segment_reassemble_batches(e2sar_hip_ctx *ctx, const e2sar_hip_seg
 {
     return segreas(ctx, batches, nBatches, lbHdrVersion, maxPldLen, stride, r, now_ms, stream);
 }
+
+#endif  // E2SAR_HIP_EXPERIMENTAL
 
 int e2sar_hip_relay_plan(e2sar_hip_reas *r, uint32_t firstRecord, uint32_t maxEvents, size_t maxPldLen,
                          uint64_t lbTick, uint16_t entropyBase, e2sar_hip_seg_event *d_events, uint32_t *d_counts,

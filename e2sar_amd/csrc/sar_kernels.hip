@@ -1285,9 +1285,12 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
     uint32_t g0 = g * G;
     uint32_t gn = (n - g0 < G) ? n - g0 : G;
     if (starts) {
+        // a caller-supplied device table: never trust it past the batch
         g0 = starts[g];
-        gn = starts[g + 1] - g0;
-        if (gn == 0u || gn > 64u) return;                            // empty stripe (host-checked <= 64)
+        if (g0 >= n) return;
+        const uint32_t g1 = (starts[g + 1] < n) ? starts[g + 1] : n;
+        if (g1 <= g0 || g1 - g0 > 64u) return;                       // empty or oversized group
+        gn = g1 - g0;
     }
     reas_range<U, HO>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
 }
@@ -1370,6 +1373,7 @@ __global__ __launch_bounds__(kBlock) void reas_keys_kernel(ReasDev R, const uint
 // reassembly groups start while the last segmentation blocks finish (no kernel boundary,
 // no half-empty tail between the two kernels).
 
+#if E2SAR_HIP_EXPERIMENTAL
 __device__ __forceinline__ void wait_group_ready(const ReasDev &R, uint32_t *tiles, uint32_t g, uint32_t expect)
 {
     if (threadIdx.x == 0) {
@@ -1416,6 +1420,8 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(C
     wait_group_ready(R, B.tiles, g, slots * (stride >> 4));
     reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L, nullptr);
 }
+
+#endif  // E2SAR_HIP_EXPERIMENTAL
 
 // ---------------------------------------------------------------------------------
 // reassembly as two phases: classify (headers only, latency-bound) then scatter (bytes
@@ -2511,6 +2517,7 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
     return hipGetLastError();
 }
 
+#if E2SAR_HIP_EXPERIMENTAL
 hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                                     uint32_t n, const uint32_t *starts, uint32_t nGroups, uint64_t now,
                                     hipStream_t stream)
@@ -2544,6 +2551,8 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
                        R, now);
     return hipGetLastError();
 }
+
+#endif  // E2SAR_HIP_EXPERIMENTAL
 
 hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                                 uint32_t n, uint64_t now, void *work, hipStream_t stream)

@@ -7,6 +7,11 @@
 
 #include "e2sar_hip.h"
 
+// launch forms kept for A/B only (include/e2sar_hip_experimental.h; `make experimental`)
+#ifndef E2SAR_HIP_EXPERIMENTAL
+#define E2SAR_HIP_EXPERIMENTAL 0
+#endif
+
 namespace e2sar_amd {
 
 // In-progress event table entry (the device form of eventsInProgress's

@@ -114,16 +114,19 @@ def exchange(send_pk: torch.Tensor, send_ln: torch.Tensor, counts: Union[Sequenc
 
 def exchange_regions(send_pk: torch.Tensor, send_ln: torch.Tensor, running: torch.Tensor, cap: int, stride: int,
                      group: Optional[dist.ProcessGroup] = None,
-                     out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
+                     out: Optional[Tuple[torch.Tensor, torch.Tensor]] = None,
+                     m: Optional[List[List[int]]] = None) -> Tuple[torch.Tensor, torch.Tensor, int]:
     """All-to-all-v of per-rank regions filled by ``RegionRouter``: rank d's datagrams are
     the first running[d] slots of region d (slots [d*cap, d*cap + running[d]) of send_pk /
     send_ln).  Split sizes from one all-gather of the running counters (one host read).
     nccl: one all_to_all over the region views (RCCL send/recv per peer, no packing copy);
     gloo: the regions are gathered on the host and sent with all_to_all_single.  Returns
-    (recv_pk, recv_ln, n_recv), received spans contiguous in source-rank order."""
+    (recv_pk, recv_ln, n_recv), received spans contiguous in source-rank order.  m: the
+    count matrix when the caller already gathered it."""
     world = dist.get_world_size(group)
     rank = dist.get_rank(group)
-    m = count_matrix(running, group)
+    if m is None:
+        m = count_matrix(running, group)
     if any(c > cap for row in m for c in row):
         raise RuntimeError(f"route regions overflowed (cap {cap} datagrams per rank): {m}")
     sc, rc = m[rank], [m[s][rank] for s in range(world)]
@@ -229,3 +232,171 @@ class PacketRouter:
             C.c_void_p(self.send_ln.data_ptr()), C.c_void_p(self.counts.data_ptr()),
             C.c_void_p(self.workspace.data_ptr()), self.workspace.numel(), C.c_void_p(_stream_handle(stream))))
         return self.send_pk, self.send_ln, self.counts
+
+
+class SpreadPipeline:
+    """BASELINE config 4 per landed batch, with the exchange overlapped.
+
+    For each batch that lands on this rank (``land``), on the caller's stream:
+
+    1. the datagrams this rank owns are reassembled where they landed (``R`` must be set to
+       this rank's ownership, ``DeviceReassembler.set_owner``), while the batch is still in
+       the Infinity Cache;
+    2. the foreign ones are appended to per-owner regions (``RegionRouter``, one launch);
+
+    then, on a communication stream, the per-owner counts are all-gathered (RCCL) and copied
+    to pinned host memory.  The host reads batch b's counts only after it has queued batch
+    b+1's landing work, then issues batch b's ``all_to_all`` of the regions (RCCL, peer to
+    peer over xGMI) on the communication stream and the reassembly of what arrived (classify
+    + scatter with streaming loads) on a third stream.  So batch b's exchange and the
+    reassembly of what it brought run while batch b+1 lands and is reassembled in place,
+    and the step costs max(landing, exchange) instead of their sum.  ``depth`` region /
+    receive buffer sets rotate; a set is reused only after the exchange and reassembly that
+    read it have finished (stream events, no host wait).
+
+    With gloo (the CPU / one-GPU rehearsal) every exchange is synchronous through host
+    memory and the received datagrams are reassembled on the caller's stream.
+
+    The reference needs no exchange: its load balancer steers every fragment of an event to
+    one receiver (e2sarDPSegmenter.hpp:231-233, e2sarDPReassembler.hpp:223-229).
+    """
+
+    def __init__(self, ctx, R, stride: int, max_batch: int, world: int, rank: int,
+                 group: Optional[dist.ProcessGroup] = None, depth: int = 2, with_lb_header: bool = True,
+                 in_place: bool = True):
+        """in_place=False routes every landed datagram, this rank's own included, through the
+        exchange (no in-place reassembly): the route-all form, which also drives the whole
+        RCCL data path at world 1."""
+        self.ctx, self.R, self.stride, self.max_batch = ctx, R, stride, max_batch
+        self.world, self.rank, self.group, self.depth = world, rank, group, depth
+        self.in_place = in_place
+        dev = ctx.torch_device
+        self.active = world > 1 or not in_place
+        self.nccl = self.active and dist.get_backend(group) == "nccl"
+        self.routers = [RegionRouter(ctx, stride, max_batch, max_batch, world, rank, with_lb_header,
+                                     foreign_only=in_place) for _ in range(depth)] if self.active else []
+        # a batch can bring at most every peer's whole batch (and its own, routing all)
+        rcap = max(1, (world - (1 if in_place else 0)) * max_batch)
+        self.recv = [(torch.empty(rcap * stride, dtype=torch.uint8, device=dev),
+                      torch.empty(rcap, dtype=torch.int32, device=dev)) for _ in range(depth)] if self.active else []
+        self.work = [R.alloc_work(rcap) for _ in range(depth)] if self.active else []
+        self.comm = torch.cuda.Stream(dev) if self.nccl else None
+        self.rx = torch.cuda.Stream(dev) if self.nccl else None
+        self.mat_dev = [torch.zeros(world * world, dtype=torch.int32, device=dev) for _ in range(depth)]
+        self.mat_host = [torch.zeros(world * world, dtype=torch.int32).pin_memory() for _ in range(depth)] \
+            if self.nccl else []
+        mk = (lambda: torch.cuda.Event()) if self.nccl else (lambda: None)
+        self.ev_routed = [mk() for _ in range(depth)]
+        self.ev_cnt = [mk() for _ in range(depth)]
+        self.ev_a2a = [mk() for _ in range(depth)]       # region set free again
+        self.ev_rx = [mk() for _ in range(depth)]        # receive set free again
+        self.used = [False] * depth
+        self.now_ms = 0
+        self.pending: List[int] = []
+        self.nb = 0
+        self.sent = 0            # foreign datagrams sent / received since begin_step
+        self.received = 0
+        self.matrices: List[List[List[int]]] = []
+        self.recv_log: List[Tuple[int, int]] = []        # (receive set, datagrams) per batch
+        # timing hook: timed(name, stream, fn, *a, **kw) -> fn(*a, stream=stream, **kw)
+        self.timed = lambda name, stream, fn, *a, **kw: fn(*a, stream=stream, **kw)
+
+    def begin_step(self) -> None:
+        self.sent = self.received = 0
+        self.matrices = []
+        self.recv_log = []
+
+    def land(self, pk: torch.Tensor, ln: torch.Tensor, n: int, now_ms: int = 0) -> None:
+        """One landed batch (on the current stream): in-place reassembly of the owned
+        datagrams, routing of the foreign ones, and the exchange pipeline's next stage."""
+        main = torch.cuda.current_stream()
+        self.now_ms = now_ms
+        if self.in_place:
+            self.timed("reas_kernel", main, self.R.reassemble, pk, self.stride, ln, n, now_ms=now_ms)
+        if not self.active:
+            return
+        slot = self.nb % self.depth
+        self.nb += 1
+        router = self.routers[slot]
+        if self.nccl and self.used[slot]:
+            main.wait_event(self.ev_a2a[slot])          # the region set's last exchange has read it
+        router.reset(stream=main)
+        self.timed("route_kernels", main, router.route, pk, ln, n)
+        self.used[slot] = True
+        if not self.nccl:
+            self._exchange_sync(slot, main)
+            return
+        self.ev_routed[slot].record(main)
+        # finish the previous batch first: collectives are issued in the same order on every
+        # rank, and its all-to-all must not queue behind this batch's count gather
+        while self.pending:
+            self._finish(self.pending.pop(0))
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.ev_routed[slot])
+            dist.all_gather_into_tensor(self.mat_dev[slot], router.running, group=self.group)
+            self.mat_host[slot].copy_(self.mat_dev[slot], non_blocking=True)
+            self.ev_cnt[slot].record(self.comm)
+        self.pending.append(slot)
+
+    def _counts(self, m: List[List[int]]):
+        if any(c > self.max_batch for row in m for c in row):
+            raise RuntimeError(f"route regions overflowed (cap {self.max_batch} datagrams per rank): {m}")
+        sc, rc = m[self.rank], [m[s][self.rank] for s in range(self.world)]
+        self.sent += sum(c for d, c in enumerate(sc) if d != self.rank)
+        self.received += sum(c for s, c in enumerate(rc) if s != self.rank)
+        self.matrices.append(m)
+        return sc, rc
+
+    def _finish(self, slot: int) -> None:
+        """Batch of region set `slot`: read its counts (host), exchange, reassemble arrivals."""
+        self.ev_cnt[slot].synchronize()
+        flat = self.mat_host[slot].tolist()
+        W = self.world
+        m = [flat[s * W:(s + 1) * W] for s in range(W)]
+        sc, rc = self._counts(m)
+        router = self.routers[slot]
+        rpk, rln = self.recv[slot]
+        n_recv = sum(rc)
+        st = self.stride
+        cap = self.max_batch
+        roff = [sum(rc[:s]) for s in range(W)]
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.ev_rx[slot])       # the receive set's last reassembly has read it
+            if any(any(row) for row in m):
+                def a2a(stream=None):
+                    dist.all_to_all([rpk[roff[s] * st:(roff[s] + rc[s]) * st] for s in range(W)],
+                                    [router.send_pk[d * cap * st:(d * cap + sc[d]) * st] for d in range(W)],
+                                    group=self.group)
+                    dist.all_to_all([rln[roff[s]:roff[s] + rc[s]] for s in range(W)],
+                                    [router.send_ln[d * cap:d * cap + sc[d]] for d in range(W)], group=self.group)
+                self.timed("exchange", self.comm, a2a)
+            self.ev_a2a[slot].record(self.comm)
+        self.recv_log.append((slot, n_recv))
+        if n_recv:
+            self.rx.wait_event(self.ev_a2a[slot])
+            self._reassemble_received(rpk, rln, n_recv, self.work[slot], self.rx)
+        self.ev_rx[slot].record(self.rx)
+
+    def _reassemble_received(self, rpk, rln, n, work, stream) -> None:
+        self.timed("reas_classify_kernel", stream, self.R.classify, rpk, self.stride, rln, n, work,
+                   now_ms=self.now_ms)
+        self.timed("reas_scatter_kernel", stream, self.R.scatter, rpk, self.stride, n, work)
+
+    def _exchange_sync(self, slot: int, main) -> None:
+        router = self.routers[slot]
+        m = count_matrix(router.running, self.group)
+        self._counts(m)
+        rpk, rln, n = exchange_regions(router.send_pk, router.send_ln, router.running, self.max_batch,
+                                       self.stride, self.group, out=self.recv[slot], m=m)
+        self.recv_log.append((slot, n))
+        if n:
+            self._reassemble_received(rpk, rln, n, self.work[slot], main)
+
+    def flush(self) -> None:
+        """Finish every batch's exchange and reassembly; the current stream waits for them."""
+        while self.pending:
+            self._finish(self.pending.pop(0))
+        if self.nccl:
+            main = torch.cuda.current_stream()
+            main.wait_stream(self.comm)
+            main.wait_stream(self.rx)

@@ -144,6 +144,7 @@ class DeviceSegmenter:
         cap = units + 2
         starts = (C.c_uint32 * cap)()
         ng = C.c_uint32()
+        _capi.need_experimental("DeviceSegmenter.groups")
         check(lib().e2sar_hip_seg_groups(plan.host, plan.n_events, plan.max_packets_per_event, self.max_pld,
                                          self.stride, starts, cap, C.byref(ng)))
         if ng.value == 0:
@@ -175,6 +176,7 @@ class DeviceSegmenter:
         in one launch (e2sar_hip_segment_reassemble_batch)."""
         if packets.numel() < plan.total_packets * self.stride or lens.numel() < plan.total_packets:
             raise ValueError("packet buffer too small")
+        _capi.need_experimental("DeviceSegmenter.segment_reassemble")
         check(lib().e2sar_hip_segment_reassemble_batch(
             self.ctx.handle, C.c_void_p(plan.device.data_ptr()), plan.n_events, plan.max_packets_per_event,
             plan.total_packets, self.lb_hdr_version, self.max_pld, C.c_void_p(packets.data_ptr()), self.stride,
@@ -192,6 +194,7 @@ class DeviceSegmenter:
                 raise ValueError("packet buffer too small")
             arr[k] = _capi.SegReasBatch(p.device.data_ptr(), pk.data_ptr(), ln.data_ptr(), p.n_events,
                                         p.max_packets_per_event, p.total_packets, 0)
+        _capi.need_experimental("DeviceSegmenter.segment_reassemble_batches")
         check(lib().e2sar_hip_segment_reassemble_batches(
             self.ctx.handle, arr, len(plans), self.lb_hdr_version, self.max_pld, self.stride, reas._h, int(now_ms),
             C.c_void_p(_stream_handle(stream))))
@@ -271,6 +274,7 @@ class DeviceReassembler:
             raise ValueError("packet batch buffers too small")
         if starts is not None and starts.numel() < n_groups + 1:
             raise ValueError("group table too small")
+        _capi.need_experimental("DeviceReassembler.reassemble_groups")
         check(lib().e2sar_hip_reassemble_groups(
             self._h, C.c_void_p(packets.data_ptr()), stride, C.c_void_p(lens.data_ptr()), n,
             C.c_void_p(starts.data_ptr() if starts is not None else 0), n_groups if starts is not None else 0,

@@ -247,8 +247,7 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
  * returns it, cpp:321).  now_ms stamps firstSegment for new events (hpp:97).
  * One fused launch for batches of up to 320 MiB of slots; above that (a batch that cannot
  * sit in the Infinity Cache) classify + scatter launches through an internal work buffer.
- * Internal buffers (this form, reference order, the chained form's counters) are kept
- * per stream, so batches may be launched on several streams at once; they grow on first
+ * Internal buffers (this form, reference order) are kept per stream, so batches may be launched on several streams at once; they grow on first
  * use for a size, never inside a graph capture (LOGIC error: run one batch of the largest
  * size on the stream first), and an outgrown buffer stays allocated until destroy, so a
  * graph captured earlier keeps valid addresses.
@@ -256,26 +255,6 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r);
 int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
                                const uint32_t *d_lens, uint32_t nPackets, uint64_t now_ms,
                                void *stream);
-
-/* Device-local round trips (a batch this library segmented is reassembled on the same GPU:
- * loopback, relay, the device-resident benchmark).  e2sar_hip_segment_batch writes its
- * datagrams in XCD stripes (runs of about one reassembly group of consecutive datagrams,
- * all written on one of the eight XCDs); e2sar_hip_seg_groups returns, for the same planned
- * host event table (pktBase filled by e2sar_hip_seg_plan), maxPacketsPerEvent, maxPldLen and
- * stride, the reassembly groups that match them: group g = datagrams [starts[g],
- * starts[g+1]) of the batch (at most 64), starts[0..*nGroups], *nGroups + 1 <= cap.
- * *nGroups = 0 when the batch has no stripes (a group would exceed 64 datagrams).
- * e2sar_hip_reassemble_groups is e2sar_hip_reassemble_batch with those groups (d_starts:
- * the table copied to the device): workgroup g reassembles group g on the XCD that wrote
- * it.  Results are those of e2sar_hip_reassemble_batch for any group table that covers
- * [0, nPackets) in order; only the fused form takes groups (a batch above 320 MiB of slots,
- * or reference-order mode, is reassembled as e2sar_hip_reassemble_batch does).  The
- * datagrams' receive body is the same: e2sarDPReassembler.cpp:335-427. */
-int e2sar_hip_seg_groups(const e2sar_hip_seg_event *events, uint32_t nEvents, uint32_t maxPacketsPerEvent,
-                         uint32_t maxPldLen, uint32_t stride, uint32_t *starts, uint32_t cap, uint32_t *nGroups);
-int e2sar_hip_reassemble_groups(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_t stride,
-                                const uint32_t *d_lens, uint32_t nPackets, const uint32_t *d_starts,
-                                uint32_t nGroups, uint64_t now_ms, void *stream);
 
 /* The same work as e2sar_hip_reassemble_batch split in two phases so a caller can
  * pipeline batches: classify (headers only: validate, look up / create, count) writes
@@ -333,40 +312,6 @@ int e2sar_hip_reas_compact(e2sar_hip_reas *r, void *stream);
 /* Zero the statistics counters (event counters, per-datagram counters, error flags).
  * Completed and lost records not yet polled stay queued.  Asynchronous. */
 int e2sar_hip_reas_reset_stats(e2sar_hip_reas *r, void *stream);
-
-/* Chained round trip (BASELINE config 2's device-resident step) in ONE launch: segment
- * the batch (as e2sar_hip_segment_batch, d_lens required) and reassemble the same
- * nPackets datagrams into r (as e2sar_hip_reassemble_batch).  Reassembly workgroups start
- * as soon as the segmentation workgroups that write their datagrams have published them
- * (write-through stores + per-group agent-scope counters held by r), so the two stages
- * overlap at their seam instead of meeting at a kernel boundary.  Results are those of
- * the two calls in sequence.  nPackets = seg_plan's total; r created withLBHeader, not
- * REFERENCE_ORDER.  The first call for a larger nPackets allocates r's counters
- * (synchronous; outside graph capture).  A group whose datagrams never all arrive (a bad
- * descriptor table) stops waiting after 2 s and sets errorFlags bit 4.  Asynchronous.
- * Replaces _send (e2sarDPSegmenter.cpp:660-871) followed by the receive body
- * (e2sarDPReassembler.cpp:335-427) on the same events. */
-int e2sar_hip_segment_reassemble_batch(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, uint32_t nEvents,
-                                       uint32_t maxPacketsPerEvent, uint32_t nPackets, int lbHdrVersion,
-                                       uint32_t maxPldLen, uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
-                                       e2sar_hip_reas *r, uint64_t now_ms, void *stream);
-
-/* Several batches (at most 8) chained in one launch: batch b's reassembly groups wait on
- * batch b's segmentation only, and batch b+1's segmentation starts while batch b's
- * reassembly finishes.  Each batch needs its own packet and length buffers.  Results are
- * those of the batches' segment_batch + reassemble_batch calls in order. */
-typedef struct e2sar_hip_segreas_batch {
-    const e2sar_hip_seg_event *d_events;   /* descriptors on the device, pktBase from seg_plan */
-    uint8_t *d_packets;
-    uint32_t *d_lens;
-    uint32_t nEvents;
-    uint32_t maxPacketsPerEvent;
-    uint32_t nPackets;
-    uint32_t reserved;
-} e2sar_hip_segreas_batch;
-int e2sar_hip_segment_reassemble_batches(e2sar_hip_ctx *ctx, const e2sar_hip_segreas_batch *batches,
-                                         uint32_t nBatches, int lbHdrVersion, uint32_t maxPldLen, uint32_t stride,
-                                         e2sar_hip_reas *r, uint64_t now_ms, void *stream);
 
 /* ------------------------------------------------------------------ */
 /* relay (BASELINE config 5: receive -> reassemble -> segment -> send on one GPU): the    */

@@ -13,8 +13,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HEADER = os.path.join(ROOT, "include", "e2sar_hip.h")
 
 
-def declared_functions():
-    src = open(HEADER).read()
+def declared_functions(header=HEADER):
+    src = open(header).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
     return sorted(set(re.findall(r"\b(e2sar_hip_[a-z0-9_]+)\s*\(", src)))
 
@@ -35,6 +35,19 @@ def test_library_exports_every_declared_symbol():
     out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True).stdout
     exported = set(re.findall(r" T (e2sar_hip_\w+)", out))
     assert set(declared_functions()) <= exported
+
+
+def test_experimental_forms_are_not_in_the_product():
+    # the A/B-only launch forms (no gain on any BASELINE config) live in
+    # e2sar_hip_experimental.h and build/variants/lib_experimental.so only
+    from e2sar_amd import _capi
+    exp = declared_functions(os.path.join(ROOT, "include", "e2sar_hip_experimental.h"))
+    assert set(exp) == set(_capi.EXPERIMENTAL_SIGNATURES)
+    assert not set(exp) & set(declared_functions())
+    out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(re.findall(r" T (e2sar_hip_\w+)", out))
+    if _capi.LIB_PATH.endswith("lib/libe2sar_hip.so"):
+        assert not set(exp) & exported
 
 
 def test_host_geometry_matches_oracle():

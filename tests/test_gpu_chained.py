@@ -13,7 +13,16 @@ import pytest
 
 import oracle_ffi as O
 
-pytestmark = pytest.mark.gpu
+def _experimental():
+    try:
+        from e2sar_amd import _capi
+        return _capi.has_experimental()
+    except ImportError:
+        return False
+
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(
+    not _experimental(), reason="A/B-only form: make experimental; E2SAR_HIP_LIB=build/variants/lib_experimental.so")]
 
 STATS = ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt", "inProgress")
 

@@ -10,9 +10,13 @@ oracle's reassembly of the datagrams that rank processed:
   (e2sar_hip_reas_set_owner), route only the foreign ones (e2sar_hip_route_foreign),
   exchange them (split sizes from one all-gather of the device count vectors), reassemble
   what arrived;
-* ``regions`` (what bench.py's spread leg runs): as ``foreign``, but the landed stream
-  comes in batches, each routed into per-rank regions right after it landed
-  (e2sar_hip_route_append), and one exchange of the regions follows the last batch.
+* ``regions``: as ``foreign``, but the landed stream comes in batches, each routed into
+  per-rank regions right after it landed (e2sar_hip_route_append), and one exchange of the
+  regions follows the last batch;
+* ``pipeline`` (what bench.py's spread sub-leg runs, dist.SpreadPipeline): per batch,
+  in-place reassembly, routing, then that batch's exchange and the reassembly of what it
+  brought (on their own streams with RCCL); ``pipeline_all`` routes every datagram through
+  the exchange.
 
 Two ranks share GPU 0 over gloo (all-to-all staged through host memory; RCCL refuses two
 ranks on one device).  The RCCL branch itself runs at world 1 in a fresh child process
@@ -73,7 +77,34 @@ def _spread_rank(rank, world, mode, corrupt=True):
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, arena_bytes=1 << 22)
     hp_l = lpk[: nl * stride].view(nl, stride).cpu().numpy()
     hl_l = lln[:nl].cpu().numpy().astype(np.uint32)
-    if mode in ("foreign", "regions"):
+    if mode in ("pipeline", "pipeline_all"):
+        # dist.SpreadPipeline (bench.py's spread sub-leg): two landed batches (a cut inside
+        # events), each reassembled in place and routed, its exchange and the reassembly of
+        # what it brought on their own streams (RCCL) or synchronous (gloo); pipeline_all
+        # routes every datagram, own included, through the exchange
+        from e2sar_amd.dist import SpreadPipeline
+        in_place = mode == "pipeline"
+        if in_place:
+            R.set_owner(world, rank)
+        pipe = SpreadPipeline(ctx, R, stride, nl, world, rank, in_place=in_place)
+        R.set_cold(True)
+        pipe.begin_step()
+        cut = nl // 3 + 1
+        for a, b in ((0, cut), (cut, nl)):
+            pipe.land(lpk[a * stride:], lln[a:], b - a)
+        pipe.flush()
+        torch.cuda.synchronize()
+        nr = sum(c for _, c in pipe.recv_log)
+        rpk = torch.cat([pipe.recv[sl][0][: c * stride] for sl, c in pipe.recv_log] + [lpk[:0]])
+        rln = torch.cat([pipe.recv[sl][1][:c] for sl, c in pipe.recv_log] + [lln[:0]])
+        counts = [sum(m[rank][d] for m in pipe.matrices) for d in range(world)]
+        keep = []
+        for k in range(nl):
+            ok, _, _, _, e, _ = O.re_parse(hp_l[k, 16:36].tobytes())
+            parsable = ok and 36 <= hl_l[k] <= stride
+            keep.append(in_place and (not parsable or e % world == rank))
+        keep = np.array(keep, bool)
+    elif mode in ("foreign", "regions"):
         R.set_owner(world, rank)
         if mode == "foreign":
             R.reassemble(lpk, stride, lln, nl)                # this rank's events, in place
@@ -174,7 +205,7 @@ def _nccl_worker(port, result_q):
         rpk, rln, nr = exchange(spk, sln, [n], stride)
         out["raw"] = bool(nr == n and torch.equal(rpk[: n * stride], spk) and torch.equal(rln[:n], sln)
                           and rpk.is_cuda)
-        for mode in ("all", "foreign", "regions"):
+        for mode in ("all", "foreign", "regions", "pipeline", "pipeline_all"):
             out[mode] = _spread_rank(0, 1, mode, corrupt=False)
         # the regions path's RCCL branch (all_to_all over region views) with data in flight:
         # every datagram routed to rank 0 itself (route_append without foreign_only)
@@ -234,7 +265,7 @@ def _run(target, args, nproc, timeout=150):
     return res
 
 
-@pytest.mark.parametrize("mode", ["all", "foreign", "regions"])
+@pytest.mark.parametrize("mode", ["all", "foreign", "regions", "pipeline", "pipeline_all"])
 def test_spread_landing_route_exchange_reassemble_two_ranks(mode):
     port = _free_port()
     world = 2
@@ -245,7 +276,7 @@ def test_spread_landing_route_exchange_reassemble_two_ranks(mode):
     # 0) misses that fragment
     assert res[1][5]["badHeaderDiscards"][0] == 1 and res[0][5]["badHeaderDiscards"][0] == 0
     assert res[0][5]["inProgress"] == (1, 1) and res[1][5]["inProgress"] == (0, 0)
-    if mode != "all":
+    if mode not in ("all", "pipeline_all"):
         # nothing a rank owns is packed for itself
         assert res[0][3][0] == 0 and res[1][3][1] == 0
 
@@ -256,10 +287,14 @@ def test_rccl_exchange_world1_fresh_process():
     assert out["backend"] == "nccl"
     assert out["raw"], "RCCL all-to-all of datagram slots changed bytes"
     assert out["regions_raw"], "RCCL all_to_all of region views changed bytes"
-    for mode in ("all", "foreign", "regions"):
+    for mode in ("all", "foreign", "regions", "pipeline", "pipeline_all"):
         rank, ok, mine, counts, nr, stat_ok = out[mode]
         assert ok, (mode, mine, counts, nr, stat_ok)
         assert mine == [100 + i for i in range(13)]
+    # SpreadPipeline over RCCL: in place nothing moves; routing all, every datagram crosses
+    # the count all-gather, the all_to_all and the received-datagram streams
+    assert out["pipeline"][3] == [0] and out["pipeline"][4] == 0
+    assert out["pipeline_all"][3] == [out["pipeline_all"][4]] and out["pipeline_all"][4] > 0
     # route_batch sends every datagram to rank 0 through RCCL; foreign-only routing keeps them
     assert out["all"][3] == [out["all"][4]] and out["all"][4] > 0
     assert out["foreign"][3] == [0] and out["foreign"][4] == 0

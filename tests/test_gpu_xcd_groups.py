@@ -10,7 +10,16 @@ groups.  The receive body is e2sarDPReassembler.cpp:335-427 either way.
 import numpy as np
 import pytest
 
-pytestmark = pytest.mark.gpu
+def _experimental():
+    try:
+        from e2sar_amd import _capi
+        return _capi.has_experimental()
+    except ImportError:
+        return False
+
+
+pytestmark = [pytest.mark.gpu, pytest.mark.skipif(
+    not _experimental(), reason="A/B-only form: make experimental; E2SAR_HIP_LIB=build/variants/lib_experimental.so")]
 
 STATS = ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt", "inProgress")
 

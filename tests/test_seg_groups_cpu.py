@@ -9,6 +9,18 @@ import ctypes as C
 import pytest
 
 
+def _experimental():
+    try:
+        from e2sar_amd import _capi
+        return _capi.has_experimental()
+    except ImportError:
+        return False
+
+
+pytestmark = pytest.mark.skipif(
+    not _experimental(), reason="A/B-only form: make experimental; E2SAR_HIP_LIB=build/variants/lib_experimental.so")
+
+
 def _geom(max_pk, stride):
     spc = stride // 16
     chunks = max_pk * spc

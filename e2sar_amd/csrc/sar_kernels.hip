@@ -54,6 +54,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_ALL
+#define E2SAR_REAS_ALL 0            // reas_kernel A/B: a group's first N rounds of loads all issued before
+#endif                              // classification (no load waits behind a store); 0 = off
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -1201,11 +1204,21 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
             da_store<HO>(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
         }
     };
+#if E2SAR_REAS_ALL
+    // every load of the group's first E2SAR_REAS_ALL rounds in flight while wave 0 classifies;
+    // the stores follow with no load behind them (vmcnt retires in issue order)
+    constexpr uint32_t RS = (uint32_t)(kBlock * U);
+    u32x4 xa[E2SAR_REAS_ALL][U];
+#pragma unroll
+    for (int r = 0; r < E2SAR_REAS_ALL; r++)
+        if ((uint32_t)r * RS < nch) issue((uint32_t)r * RS, xa[r]);
+#else
     u32x4 x[U];
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
     issue(0u, x);                      // round 0 is in flight while wave 0 classifies
+#endif
 
     unsigned long long old = 0;
     if (w0) {
@@ -1225,7 +1238,15 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     lds_barrier();
     TRACE_AT(0, 2, trace_hwid());
 
-#if E2SAR_REAS_PIPE
+#if E2SAR_REAS_ALL
+#pragma unroll
+    for (int r = 0; r < E2SAR_REAS_ALL; r++)
+        if ((uint32_t)r * RS < nch) store((uint32_t)r * RS, xa[r]);
+    for (uint32_t r0 = (uint32_t)E2SAR_REAS_ALL * RS; r0 < nch; r0 += RS) {     // groups past the budget
+        issue(r0, xa[0]);
+        store(r0, xa[0]);
+    }
+#elif E2SAR_REAS_PIPE
     // software pipeline: the loads of round r+1 are issued before the stores of round r.
     // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
     // a store can only be waited for together with that store's write acknowledgement;

@@ -32,8 +32,10 @@ def owner(event_num: int, world: int) -> int:
 
 
 def _via_host(group, t: torch.Tensor) -> bool:
-    """gloo's collectives take host tensors: device tensors are staged through host memory."""
-    return dist.get_backend(group) == "gloo" and t.is_cuda
+    """gloo's collectives take host tensors (device tensors are staged through host memory)
+    and have no list all-to-all: with gloo every exchange goes through all_to_all_single on
+    host tensors."""
+    return dist.get_backend(group) == "gloo"
 
 
 def count_matrix(counts: torch.Tensor, group: Optional[dist.ProcessGroup] = None) -> List[List[int]]:
@@ -309,7 +311,7 @@ class SpreadPipeline:
     def land(self, pk: torch.Tensor, ln: torch.Tensor, n: int, now_ms: int = 0) -> None:
         """One landed batch (on the current stream): in-place reassembly of the owned
         datagrams, routing of the foreign ones, and the exchange pipeline's next stage."""
-        main = torch.cuda.current_stream()
+        main = torch.cuda.current_stream() if torch.cuda.is_available() else None
         self.now_ms = now_ms
         if self.in_place:
             self.timed("reas_kernel", main, self.R.reassemble, pk, self.stride, ln, n, now_ms=now_ms)

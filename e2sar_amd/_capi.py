@@ -234,9 +234,22 @@ def lib() -> C.CDLL:
 
 
 def has_experimental() -> bool:
-    """True when the loaded library carries the A/B-only forms of e2sar_hip_experimental.h."""
-    L = lib()
-    return all(hasattr(L, n) for n in EXPERIMENTAL_SIGNATURES)
+    """True when the library carries the A/B-only forms of e2sar_hip_experimental.h.
+
+    Reads the library's dynamic symbol table without loading it: in a process that also
+    uses PyTorch, the library must be loaded only after torch has initialised the GPU (its
+    HIP runtime and torch's share one HSA runtime, the first one loaded; sar.Context loads
+    the library after torch.cuda.set_device).  Loaded first, this library's runtime finds no
+    device.  So a test module's skip marker, evaluated at collection, must not load it."""
+    if _lib is not None:
+        return all(hasattr(_lib, n) for n in EXPERIMENTAL_SIGNATURES)
+    import subprocess
+    try:
+        out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True,
+                             timeout=30).stdout
+    except (OSError, subprocess.SubprocessError):
+        return False
+    return all(f" T {n}\n" in out + "\n" for n in EXPERIMENTAL_SIGNATURES)
 
 
 def need_experimental(what: str) -> None:

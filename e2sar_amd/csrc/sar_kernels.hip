@@ -57,6 +57,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_ALL
 #define E2SAR_REAS_ALL 0            // reas_kernel A/B: a group's first N rounds of loads all issued before
 #endif                              // classification (no load waits behind a store); 0 = off
+#ifndef E2SAR_REAS_READ_FIRST
+#define E2SAR_REAS_READ_FIRST 0     // find_or_create A/B: first pass reads records A/B (one uncontended
+#endif                              // load) and claims only a slot it finds EMPTY; 0 = claim first
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -613,6 +616,9 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
     uint32_t pass = 0;
 #endif
     bool claimed = false;          // the current slot is known to be past EMPTY: poll by loads
+#if E2SAR_REAS_READ_FIRST
+    bool peeked = false;           // records A/B of this slot were read once: EMPTY -> claim now
+#endif
     while (__ballot(active)) {
         bool waiting = false, advance = false;
         if (active) {
@@ -620,7 +626,26 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             // a slot never returns to EMPTY within an arena epoch, so once a claim has
             // failed, later passes poll records A/B with loads instead of repeating the CAS
             // (A/B: +1.1 % at 1 MiB / MTU 1500, +1.8 % at 8 MiB / MTU 9000)
+#if E2SAR_REAS_READ_FIRST
+            // read first: a lookup of an event that exists costs one load, not a contended CAS
+            uint32_t old;
+            u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
+            bool haveAB = false;
+            if (!claimed && !peeked) {
+                ld_slot_ab(sl, A0, B0);
+                peeked = true;
+                if (A0.x == kEmpty) {
+                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+                } else {
+                    old = kBusy;              // examined below from the records just read
+                    haveAB = true;
+                }
+            } else {
+                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+            }
+#else
             const uint32_t old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+#endif
 #if E2SAR_TRACE
             if (pass == 0) {
                 TRACE_WAIT();
@@ -652,7 +677,16 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             } else if (old == kBusy || old == kReady) {
                 u32x4 A, B;
+#if E2SAR_REAS_READ_FIRST
+                if (haveAB) {
+                    A = A0;
+                    B = B0;
+                } else {
+                    ld_slot_ab(sl, A, B);
+                }
+#else
                 ld_slot_ab(sl, A, B);
+#endif
                 if (A.x == kReady && B.w != 0u) {
                     if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
                         res.slot = h;
@@ -673,6 +707,9 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             }
             if (advance) {
                 claimed = false;
+#if E2SAR_REAS_READ_FIRST
+                peeked = false;
+#endif
                 h = (h + 1u) & mask;
                 if (++probes >= R.tableSlots) {
                     atomicOr(&R.ctl->errorFlags, 1u);

@@ -388,8 +388,13 @@ class SpreadPipeline:
         router = self.routers[slot]
         m = count_matrix(router.running, self.group)
         self._counts(m)
-        rpk, rln, n = exchange_regions(router.send_pk, router.send_ln, router.running, self.max_batch,
-                                       self.stride, self.group, out=self.recv[slot], m=m)
+        res = []
+
+        def ex(stream=None):
+            res.append(exchange_regions(router.send_pk, router.send_ln, router.running, self.max_batch,
+                                        self.stride, self.group, out=self.recv[slot], m=m))
+        self.timed("exchange", main, ex)
+        rpk, rln, n = res[0]
         self.recv_log.append((slot, n))
         if n:
             self._reassemble_received(rpk, rln, n, self.work[slot], main)

@@ -21,7 +21,4 @@ for rep in 1 2; do
 import json; d=json.loads(open('$O/r2_$rep.json').read().strip().splitlines()[-1]); print('r2', d['value'], d['roofline']['avg_launch_ms'])" >> $O/knobs.log
 done
 cat $O/knobs.log
-timeout -k 10 400 python bench.py > $O/bench_default.json 2> $O/bench_default.err || { echo "bench failed"; tail -20 $O/bench_default.err; exit 1; }
-tools/profile_round4.sh $O/prof headline cold mtu9000 config3 || { echo "profile failed"; tail $O/prof/progress.log; exit 1; }
-tools/c3_bimodal.sh $O/c3 5 > $O/c3.log 2>&1 || { echo "c3 failed"; tail $O/c3.log; exit 1; }
 echo done

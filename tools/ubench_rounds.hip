@@ -234,6 +234,30 @@ __global__ __launch_bounds__(256) void dg_naive(const uint8_t *slots, uint8_t *d
     }
 }
 
+// rounds aligned to datagram boundaries: round k covers datagrams [11k, 11k + 11) (1012 of
+// 1024 lanes), so no datagram straddles two rounds
+template <int G>
+__global__ __launch_bounds__(256) void dg_rows(const uint8_t *slots, uint8_t *dst, uint32_t n)
+{
+    const uint32_t pg = blockIdx.x * G;
+    const uint32_t gn = (n - pg < G) ? n - pg : G;
+    const uint8_t *s = slots + (uint64_t)pg * kStride;
+    for (uint32_t q0 = 0; q0 < gn; q0 += 11) {
+        const uint32_t qn = (gn - q0 < 11) ? gn - q0 : 11;
+        const uint32_t nch = qn * kSpc;
+        u32x4 x[4];
+        DgChunk d[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            d[u] = dg_split(u * 256 + threadIdx.x, nch);
+            d[u].p += q0;
+            x[u] = dg_load(s, pg, d[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) dg_store(dst, pg, d[u], x[u]);
+    }
+}
+
 template <int G>
 __global__ __launch_bounds__(256) void dg_pipe(const uint8_t *slots, uint8_t *dst, uint32_t n)
 {
@@ -364,6 +388,14 @@ int main(int argc, char **argv)
         printf(", \"all49\": %.2f", timedg([&] { dg_all<49, 5><<<NG(49), 256>>>(slots, dst, n); }));
         printf(", \"all33\": %.2f", timedg([&] { dg_all<33, 3><<<NG(33), 256>>>(slots, dst, n); }));
         printf(", \"pipe22\": %.2f", timedg([&] { dg_pipe<22><<<NG(22), 256>>>(slots, dst, n); }));
+        printf(", \"naive16\": %.2f", timedg([&] { dg_naive<16><<<NG(16), 256>>>(slots, dst, n); }));
+        printf(", \"naive24\": %.2f", timedg([&] { dg_naive<24><<<NG(24), 256>>>(slots, dst, n); }));
+        printf(", \"naive32\": %.2f", timedg([&] { dg_naive<32><<<NG(32), 256>>>(slots, dst, n); }));
+        printf(", \"rows44\": %.2f", timedg([&] { dg_rows<44><<<NG(44), 256>>>(slots, dst, n); }));
+        printf(", \"rows22\": %.2f", timedg([&] { dg_rows<22><<<NG(22), 256>>>(slots, dst, n); }));
+        // the fused kernel's residency (6 workgroups per CU): 24 KiB of dynamic LDS each
+        printf(", \"one8_occ6\": %.2f", timedg([&] { dg_naive<8><<<NG(8), 256, 24576>>>(slots, dst, n); }));
+        printf(", \"pipe49_occ6\": %.2f", timedg([&] { dg_pipe<49><<<NG(49), 256, 24576>>>(slots, dst, n); }));
         printf("}");
     }
     printf("}\n");

@@ -57,6 +57,9 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_ALL
 #define E2SAR_REAS_ALL 0            // reas_kernel A/B: a group's first N rounds of loads all issued before
 #endif                              // classification (no load waits behind a store); 0 = off
+#ifndef E2SAR_REAS_EARLY2
+#define E2SAR_REAS_EARLY2 0         // reas_kernel A/B: rounds 0 and 1 in flight during classification
+#endif
 #ifndef E2SAR_REAS_READ_FIRST
 #define E2SAR_REAS_READ_FIRST 0     // find_or_create A/B: first pass reads records A/B (one uncontended
 #endif                              // load) and claims only a slot it finds EMPTY; 0 = claim first
@@ -1255,6 +1258,10 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     u32x4 y[U];
 #endif
     issue(0u, x);                      // round 0 is in flight while wave 0 classifies
+#if E2SAR_REAS_PIPE && E2SAR_REAS_EARLY2
+    constexpr uint32_t RS = (uint32_t)(kBlock * U);
+    if (RS < nch) issue(RS, y);        // A/B: round 1 in flight during classification too
+#endif
 #endif
 
     unsigned long long old = 0;
@@ -1288,8 +1295,10 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
     // a store can only be waited for together with that store's write acknowledgement;
     // issued before it, round r+1's data is waited for while round r's stores drain.
+#if !E2SAR_REAS_EARLY2
     constexpr uint32_t RS = (uint32_t)(kBlock * U);
     if (RS < nch) issue(RS, y);
+#endif
     store(0u, x);
     for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
         if (r0 + RS < nch) issue(r0 + RS, x);

@@ -54,15 +54,6 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
-#ifndef E2SAR_REAS_ALL
-#define E2SAR_REAS_ALL 0            // reas_kernel A/B: a group's first N rounds of loads all issued before
-#endif                              // classification (no load waits behind a store); 0 = off
-#ifndef E2SAR_REAS_EARLY2
-#define E2SAR_REAS_EARLY2 0         // reas_kernel A/B: rounds 0 and 1 in flight during classification
-#endif
-#ifndef E2SAR_REAS_READ_FIRST
-#define E2SAR_REAS_READ_FIRST 0     // find_or_create A/B: first pass reads records A/B (one uncontended
-#endif                              // load) and claims only a slot it finds EMPTY; 0 = claim first
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -619,9 +610,6 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
     uint32_t pass = 0;
 #endif
     bool claimed = false;          // the current slot is known to be past EMPTY: poll by loads
-#if E2SAR_REAS_READ_FIRST
-    bool peeked = false;           // records A/B of this slot were read once: EMPTY -> claim now
-#endif
     while (__ballot(active)) {
         bool waiting = false, advance = false;
         if (active) {
@@ -629,26 +617,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             // a slot never returns to EMPTY within an arena epoch, so once a claim has
             // failed, later passes poll records A/B with loads instead of repeating the CAS
             // (A/B: +1.1 % at 1 MiB / MTU 1500, +1.8 % at 8 MiB / MTU 9000)
-#if E2SAR_REAS_READ_FIRST
-            // read first: a lookup of an event that exists costs one load, not a contended CAS
-            uint32_t old;
-            u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
-            bool haveAB = false;
-            if (!claimed && !peeked) {
-                ld_slot_ab(sl, A0, B0);
-                peeked = true;
-                if (A0.x == kEmpty) {
-                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-                } else {
-                    old = kBusy;              // examined below from the records just read
-                    haveAB = true;
-                }
-            } else {
-                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-            }
-#else
             const uint32_t old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-#endif
 #if E2SAR_TRACE
             if (pass == 0) {
                 TRACE_WAIT();
@@ -680,16 +649,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             } else if (old == kBusy || old == kReady) {
                 u32x4 A, B;
-#if E2SAR_REAS_READ_FIRST
-                if (haveAB) {
-                    A = A0;
-                    B = B0;
-                } else {
-                    ld_slot_ab(sl, A, B);
-                }
-#else
                 ld_slot_ab(sl, A, B);
-#endif
                 if (A.x == kReady && B.w != 0u) {
                     if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
                         res.slot = h;
@@ -710,9 +670,6 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             }
             if (advance) {
                 claimed = false;
-#if E2SAR_REAS_READ_FIRST
-                peeked = false;
-#endif
                 h = (h + 1u) & mask;
                 if (++probes >= R.tableSlots) {
                     atomicOr(&R.ctl->errorFlags, 1u);
@@ -1244,25 +1201,11 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
             da_store<HO>(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
         }
     };
-#if E2SAR_REAS_ALL
-    // every load of the group's first E2SAR_REAS_ALL rounds in flight while wave 0 classifies;
-    // the stores follow with no load behind them (vmcnt retires in issue order)
-    constexpr uint32_t RS = (uint32_t)(kBlock * U);
-    u32x4 xa[E2SAR_REAS_ALL][U];
-#pragma unroll
-    for (int r = 0; r < E2SAR_REAS_ALL; r++)
-        if ((uint32_t)r * RS < nch) issue((uint32_t)r * RS, xa[r]);
-#else
     u32x4 x[U];
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
     issue(0u, x);                      // round 0 is in flight while wave 0 classifies
-#if E2SAR_REAS_PIPE && E2SAR_REAS_EARLY2
-    constexpr uint32_t RS = (uint32_t)(kBlock * U);
-    if (RS < nch) issue(RS, y);        // A/B: round 1 in flight during classification too
-#endif
-#endif
 
     unsigned long long old = 0;
     if (w0) {
@@ -1282,23 +1225,13 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     lds_barrier();
     TRACE_AT(0, 2, trace_hwid());
 
-#if E2SAR_REAS_ALL
-#pragma unroll
-    for (int r = 0; r < E2SAR_REAS_ALL; r++)
-        if ((uint32_t)r * RS < nch) store((uint32_t)r * RS, xa[r]);
-    for (uint32_t r0 = (uint32_t)E2SAR_REAS_ALL * RS; r0 < nch; r0 += RS) {     // groups past the budget
-        issue(r0, xa[0]);
-        store(r0, xa[0]);
-    }
-#elif E2SAR_REAS_PIPE
+#if E2SAR_REAS_PIPE
     // software pipeline: the loads of round r+1 are issued before the stores of round r.
     // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
     // a store can only be waited for together with that store's write acknowledgement;
     // issued before it, round r+1's data is waited for while round r's stores drain.
-#if !E2SAR_REAS_EARLY2
     constexpr uint32_t RS = (uint32_t)(kBlock * U);
     if (RS < nch) issue(RS, y);
-#endif
     store(0u, x);
     for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
         if (r0 + RS < nch) issue(r0 + RS, x);

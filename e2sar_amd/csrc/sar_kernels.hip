@@ -54,9 +54,6 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
-#ifndef E2SAR_REAS_W0_LATE
-#define E2SAR_REAS_W0_LATE 1        // reas_kernel: wave 0 issues its round-0 payload loads after it classified
-#endif
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -1208,11 +1205,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
-    // round 0 is in flight while wave 0 classifies -- but wave 0's own share is issued only
-    // after its classification (E2SAR_REAS_W0_LATE): vmcnt retires in issue order, so every
-    // table round trip of wave 0 (the claim, the record reads) would otherwise wait for its
-    // payload loads as well
-    if (!(E2SAR_REAS_W0_LATE && w0)) issue(0u, x);
+    issue(0u, x);                      // round 0 is in flight while wave 0 classifies
 
     unsigned long long old = 0;
     if (w0) {
@@ -1228,7 +1221,6 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
         L.rc[lane] = cl.rc;
         L.tail[lane] = cl.tailAdd ? 1u : 0u;
         TRACE_AT(0, 1, trace_now());
-        if (E2SAR_REAS_W0_LATE) issue(0u, x);
     }
     lds_barrier();
     TRACE_AT(0, 2, trace_hwid());

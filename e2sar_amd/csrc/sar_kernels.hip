@@ -54,6 +54,12 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_LOOKUP_FIRST
+#define E2SAR_REAS_LOOKUP_FIRST 1   // reas_kernel: wave 0's first table operation before its round-0 loads
+#endif
+#ifndef E2SAR_REAS_READ_FIRST
+#define E2SAR_REAS_READ_FIRST 0     // find_or_create A/B: first pass reads records A/B (one uncontended
+#endif                              // load) and claims only a slot it finds EMPTY; 0 = claim first
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -610,6 +616,9 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
     uint32_t pass = 0;
 #endif
     bool claimed = false;          // the current slot is known to be past EMPTY: poll by loads
+#if E2SAR_REAS_READ_FIRST
+    bool peeked = false;           // records A/B of this slot were read once: EMPTY -> claim now
+#endif
     while (__ballot(active)) {
         bool waiting = false, advance = false;
         if (active) {
@@ -617,7 +626,26 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             // a slot never returns to EMPTY within an arena epoch, so once a claim has
             // failed, later passes poll records A/B with loads instead of repeating the CAS
             // (A/B: +1.1 % at 1 MiB / MTU 1500, +1.8 % at 8 MiB / MTU 9000)
+#if E2SAR_REAS_READ_FIRST
+            // read first: a lookup of an event that exists costs one load, not a contended CAS
+            uint32_t old;
+            u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
+            bool haveAB = false;
+            if (!claimed && !peeked) {
+                ld_slot_ab(sl, A0, B0);
+                peeked = true;
+                if (A0.x == kEmpty) {
+                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+                } else {
+                    old = kBusy;              // examined below from the records just read
+                    haveAB = true;
+                }
+            } else {
+                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+            }
+#else
             const uint32_t old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+#endif
 #if E2SAR_TRACE
             if (pass == 0) {
                 TRACE_WAIT();
@@ -649,7 +677,16 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             } else if (old == kBusy || old == kReady) {
                 u32x4 A, B;
+#if E2SAR_REAS_READ_FIRST
+                if (haveAB) {
+                    A = A0;
+                    B = B0;
+                } else {
+                    ld_slot_ab(sl, A, B);
+                }
+#else
                 ld_slot_ab(sl, A, B);
+#endif
                 if (A.x == kReady && B.w != 0u) {
                     if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
                         res.slot = h;
@@ -670,6 +707,9 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             }
             if (advance) {
                 claimed = false;
+#if E2SAR_REAS_READ_FIRST
+                peeked = false;
+#endif
                 h = (h + 1u) & mask;
                 if (++probes >= R.tableSlots) {
                     atomicOr(&R.ctl->errorFlags, 1u);
@@ -681,6 +721,147 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             }
         }
+        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
+#if E2SAR_TRACE
+        pass++;
+#endif
+    }
+#if E2SAR_TRACE
+    if (__ballot(want)) {
+        TRACE_FIRST(2, 2, trace_now());
+        TRACE_FIRST(2, 3, pass);
+    }
+#endif
+    return res;
+}
+
+// The fused kernel's lookup (reas_range): the same protocol as find_or_create, with the
+// first table operation of every wanting lane (the claim, or with E2SAR_REAS_READ_FIRST the
+// read of records A/B) issued BEFORE `pre` -- the caller's round-0 payload loads, issued by
+// the whole wave -- so that waiting for it does not wait for those loads too (vmcnt retires
+// in issue order).  Records A/B are read with compiler-counted sc1 buffer loads (volatile:
+// never hoisted out of the poll loop), so each wait is only as deep as it must be.
+struct NoPre {
+    __device__ void operator()() const {}
+};
+constexpr int kCpolVolatile = (int)(1u << 31);
+__device__ __forceinline__ void ld_slot_ab_rs(__amdgpu_buffer_rsrc_t rs, uint32_t h, u32x4 &A, u32x4 &B)
+{
+    A = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot)), 0, kCpolSc1 | kCpolVolatile);
+    B = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot) + 16u), 0,
+                                              kCpolSc1 | kCpolVolatile);
+}
+template <typename Pre>
+__device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
+                                           uint64_t now, const Pre &pre)
+{
+    LookupResult res{kNoSlot, 0, kNoBuf};
+    const uint32_t mask = R.tableSlots - 1u;
+    uint32_t h = slot_hash(ev, d, mask);
+    uint32_t probes = 0, spins = 0;
+    bool active = want;
+    const __amdgpu_buffer_rsrc_t rs = brsrc(R.slots);
+#if E2SAR_TRACE
+    uint32_t pass = 0;
+#endif
+    bool claimed = false;
+    // ---- the first table operation, then the caller's loads ----
+    // claim-first: the claim and a read of records A/B go out together, so a lane that finds
+    // the event already published resolves in this one round trip; read-first: the read only
+    uint32_t old0 = kBusy;
+    u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
+    if (active) {
+#if !E2SAR_REAS_READ_FIRST
+        old0 = atomicCAS(&R.slots[h].state, (uint32_t)kEmpty, (uint32_t)kBusy);
+#endif
+        ld_slot_ab_rs(rs, h, A0, B0);
+    }
+    pre();
+    bool first = true;
+    while (__ballot(active)) {
+        bool waiting = false, advance = false;
+        if (active) {
+            ReasSlot *sl = R.slots + h;
+            uint32_t old;
+            bool haveAB = false;
+            u32x4 A, B;
+            if (first) {
+#if E2SAR_REAS_READ_FIRST
+                if (A0.x == kEmpty) {
+                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+                } else {
+                    old = kBusy;
+                    A = A0;
+                    B = B0;
+                    haveAB = true;
+                }
+#else
+                old = old0;
+                if (old != kEmpty) {
+                    A = A0;
+                    B = B0;
+                    haveAB = true;
+                }
+#endif
+            } else {
+                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
+            }
+#if E2SAR_TRACE
+            if (pass == 0) {
+                TRACE_WAIT();
+                TRACE_FIRST(2, 1, trace_now());
+            }
+#endif
+            if (old == kEmpty) {
+                const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
+                uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
+                if (boff + blen > R.arenaBytes) {
+                    boff = kNoBuf;
+                    atomicOr(&R.ctl->errorFlags, 2u);
+                }
+                st_agent(&sl->created, now);
+                st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, 1u});
+                st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
+                atomicAdd(occ_in_progress(R, h), 1ull);
+                atomicAdd(occ_table_used(R, h), 1ull);
+                res.slot = h;
+                res.bytes = blen;
+                res.bufOff = boff;
+                active = false;
+            } else if (old == kBusy || old == kReady) {
+                if (!haveAB) ld_slot_ab_rs(rs, h, A, B);
+                if (A.x == kReady && B.w != 0u) {
+                    if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
+                        res.slot = h;
+                        res.bytes = B.z;
+                        res.bufOff = ((uint64_t)B.y << 32) | B.x;
+                        active = false;
+                    } else {
+                        advance = true;
+                    }
+                } else if (A.x == kDone || A.x == kLost) {
+                    advance = true;
+                } else {
+                    waiting = true;
+                    claimed = true;
+                }
+            } else {
+                advance = true;
+            }
+            if (advance) {
+                claimed = false;
+                h = (h + 1u) & mask;
+                if (++probes >= R.tableSlots) {
+                    atomicOr(&R.ctl->errorFlags, 1u);
+                    active = false;
+                }
+            }
+            if (waiting && ++spins > kSpinLimit) {
+                atomicOr(&R.ctl->errorFlags, 4u);
+                active = false;
+            }
+        }
+        first = false;
         if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
 #if E2SAR_TRACE
         pass++;
@@ -827,9 +1008,10 @@ struct Classified {
 // per-event atomics are per run, not per datagram.
 // DeferAcc: the run tail's add to the event's accumulator is left to the caller (the fused
 // kernel issues it after its copy, so the copy's waits never sit behind that atomic).
-template <bool DeferAcc = false>
+template <bool DeferAcc = false, typename Pre = NoPre>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
-                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{})
+                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{},
+                                    const Pre *pre = nullptr)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
@@ -872,19 +1054,22 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
 
     // keys resolved by the group-key pre-pass (reas_keys_kernel): a run head whose key is
     // one of them takes its slot and buffer from the record instead of the table
-    bool pre = false;
+    bool prek = false;
     LookupResult lr{kNoSlot, 0, kNoBuf};
     if (hasKeys) {
 #pragma unroll
         for (int k = 0; k < 2; k++)
-            if (!pre && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
-                pre = true;
+            if (!prek && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
+                prek = true;
                 lr = LookupResult{K.slot[k], K.bytes[k], K.boff[k]};
             }
     }
     {
-        const LookupResult lk = find_or_create(R, head && !pre, ev, d, blen, now);
-        if (!pre) lr = lk;
+        // a caller's pre-issue hook (the fused kernel's round-0 loads) goes after the first
+        // table operation; otherwise the plain lookup
+        const LookupResult lk = pre ? find_or_create_pre(R, head && !prek, ev, d, blen, now, *pre)
+                                    : find_or_create(R, head && !prek, ev, d, blen, now);
+        if (!prek) lr = lk;
     }
 
     const uint64_t H = __ballot(head);
@@ -1205,11 +1390,16 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
-    issue(0u, x);                      // round 0 is in flight while wave 0 classifies
+    // round 0 is in flight while wave 0 classifies; wave 0 issues its own share right after
+    // its first table operation (E2SAR_REAS_LOOKUP_FIRST), so that operation's round trip is
+    // not queued behind the payload loads in vmcnt order
+    if (!(E2SAR_REAS_LOOKUP_FIRST && w0)) issue(0u, x);
 
     unsigned long long old = 0;
     if (w0) {
-        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(R, raw, stride, lane < gn, now, g, key != nullptr, K);
+        auto pre0 = [&]() { issue(0u, x); };
+        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(
+            R, raw, stride, lane < gn, now, g, key != nullptr, K, E2SAR_REAS_LOOKUP_FIRST ? &pre0 : nullptr);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;

@@ -107,6 +107,15 @@ def main():
             r["first_wave_detail"] = {"headers": qf((d[:, 0] - s0) * 0.01), "first_cas": qf((d[:, 1] - d[:, 0]) * 0.01),
                                       "rest_of_lookup": qf((d[:, 2] - d[:, 1]) * 0.01),
                                       "after_lookup": qf((t[:, 1].astype(np.int64) - d[:, 2]) * 0.01)}
+            # the groups dispatched later (started 10 us or more after the first)
+            lw = okd & (st >= st.min() + 10.0)
+            r["later_blocks"] = int(lw.sum())
+            if lw.any():
+                ql = lambda v: [round(float(x), 2) for x in np.quantile(v[lw], [0.1, 0.5, 0.9])]
+                r["later_detail"] = {"headers": ql((d[:, 0] - s0) * 0.01), "first_cas": ql((d[:, 1] - d[:, 0]) * 0.01),
+                                     "rest_of_lookup": ql((d[:, 2] - d[:, 1]) * 0.01),
+                                     "after_lookup": ql((t[:, 1].astype(np.int64) - d[:, 2]) * 0.01),
+                                     "classify": ql(cl)}
         # concurrency profile: running blocks per 2 us bin
         lo, hi = float(st.min()), float(en[ok].max())
         bins = np.arange(lo, hi + 2, 2.0)

@@ -739,17 +739,18 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
 // first table operation of every wanting lane (the claim, or with E2SAR_REAS_READ_FIRST the
 // read of records A/B) issued BEFORE `pre` -- the caller's round-0 payload loads, issued by
 // the whole wave -- so that waiting for it does not wait for those loads too (vmcnt retires
-// in issue order).  Records A/B are read with compiler-counted sc1 buffer loads (volatile:
-// never hoisted out of the poll loop), so each wait is only as deep as it must be.
+// in issue order).  Records A/B are read with compiler-counted 16-byte sc1 buffer loads, the
+// cache policy of ld_slot_ab.  (Marked volatile, the compiler emits them sc0 sc1; with those,
+// one event in ~4000 of the bench's verified step never completed -- consistent with a 16-byte
+// record read torn against a concurrent publish -- so the loads are not volatile.)  The poll
+// loop holds atomics and memory-clobbering stores, so the loads cannot be hoisted out of it.
 struct NoPre {
     __device__ void operator()() const {}
 };
-constexpr int kCpolVolatile = (int)(1u << 31);
 __device__ __forceinline__ void ld_slot_ab_rs(__amdgpu_buffer_rsrc_t rs, uint32_t h, u32x4 &A, u32x4 &B)
 {
-    A = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot)), 0, kCpolSc1 | kCpolVolatile);
-    B = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot) + 16u), 0,
-                                              kCpolSc1 | kCpolVolatile);
+    A = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot)), 0, kCpolSc1);
+    B = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot) + 16u), 0, kCpolSc1);
 }
 template <typename Pre>
 __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,

@@ -736,23 +736,20 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
 }
 
 // The fused kernel's lookup (reas_range): the same protocol as find_or_create, with the
-// first table operation of every wanting lane (the claim, or with E2SAR_REAS_READ_FIRST the
-// read of records A/B) issued BEFORE `pre` -- the caller's round-0 payload loads, issued by
-// the whole wave -- so that waiting for it does not wait for those loads too (vmcnt retires
-// in issue order).  Records A/B are read with compiler-counted 16-byte sc1 buffer loads, the
-// cache policy of ld_slot_ab.  (Marked volatile, the compiler emits them sc0 sc1; with those,
-// one event in ~4000 of the bench's verified step never completed -- consistent with a 16-byte
-// record read torn against a concurrent publish -- so the loads are not volatile.)  The poll
-// loop holds atomics and memory-clobbering stores, so the loads cannot be hoisted out of it.
+// first table operation of every wanting lane (the claim and a read of records A/B, or with
+// E2SAR_REAS_READ_FIRST the read only) issued BEFORE `pre` -- the caller's round-0 payload
+// loads, kPreLoads 16-byte loads issued by the whole wave -- so that waiting for it does not
+// wait for those loads too (vmcnt retires in issue order).  The pass-0 record read is the
+// same sc1 global load as ld_slot_ab, in inline asm, waited for by a counted vmcnt that
+// leaves the caller's loads in flight (the guide's asm form (ii): the wait names both
+// destinations "+v").  (Compiler-counted sc1 buffer loads for the records were tried first:
+// with them, lookups in the bench's full batch spun for seconds and an event went missing;
+// the asm global loads the protocol has always used do not.)  Later passes poll with
+// ld_slot_ab.
 struct NoPre {
     __device__ void operator()() const {}
 };
-__device__ __forceinline__ void ld_slot_ab_rs(__amdgpu_buffer_rsrc_t rs, uint32_t h, u32x4 &A, u32x4 &B)
-{
-    A = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot)), 0, kCpolSc1);
-    B = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(h * (uint32_t)sizeof(ReasSlot) + 16u), 0, kCpolSc1);
-}
-template <typename Pre>
+template <int kPreLoads, typename Pre>
 __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
                                            uint64_t now, const Pre &pre)
 {
@@ -761,7 +758,6 @@ __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t
     uint32_t h = slot_hash(ev, d, mask);
     uint32_t probes = 0, spins = 0;
     bool active = want;
-    const __amdgpu_buffer_rsrc_t rs = brsrc(R.slots);
 #if E2SAR_TRACE
     uint32_t pass = 0;
 #endif
@@ -775,9 +771,15 @@ __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t
 #if !E2SAR_REAS_READ_FIRST
         old0 = atomicCAS(&R.slots[h].state, (uint32_t)kEmpty, (uint32_t)kBusy);
 #endif
-        ld_slot_ab_rs(rs, h, A0, B0);
+        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
+                     "global_load_dwordx4 %1, %2, off offset:16 sc1"
+                     : "=&v"(A0), "=&v"(B0)
+                     : "v"(R.slots + h)
+                     : "memory");
     }
     pre();
+    // the two record loads are older than the caller's kPreLoads loads: vmcnt(kPreLoads) has them
+    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(A0), "+v"(B0) : "n"(kPreLoads) : "memory");
     bool first = true;
     while (__ballot(active)) {
         bool waiting = false, advance = false;
@@ -830,7 +832,7 @@ __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t
                 res.bufOff = boff;
                 active = false;
             } else if (old == kBusy || old == kReady) {
-                if (!haveAB) ld_slot_ab_rs(rs, h, A, B);
+                if (!haveAB) ld_slot_ab(sl, A, B);
                 if (A.x == kReady && B.w != 0u) {
                     if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
                         res.slot = h;
@@ -1009,7 +1011,7 @@ struct Classified {
 // per-event atomics are per run, not per datagram.
 // DeferAcc: the run tail's add to the event's accumulator is left to the caller (the fused
 // kernel issues it after its copy, so the copy's waits never sit behind that atomic).
-template <bool DeferAcc = false, typename Pre = NoPre>
+template <bool DeferAcc = false, typename Pre = NoPre, int kPreLoads = 0>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
                                     uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{},
                                     const Pre *pre = nullptr)
@@ -1068,7 +1070,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     {
         // a caller's pre-issue hook (the fused kernel's round-0 loads) goes after the first
         // table operation; otherwise the plain lookup
-        const LookupResult lk = pre ? find_or_create_pre(R, head && !prek, ev, d, blen, now, *pre)
+        const LookupResult lk = pre ? find_or_create_pre<kPreLoads>(R, head && !prek, ev, d, blen, now, *pre)
                                     : find_or_create(R, head && !prek, ev, d, blen, now);
         if (!prek) lr = lk;
     }
@@ -1398,8 +1400,8 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 
     unsigned long long old = 0;
     if (w0) {
-        auto pre0 = [&]() { issue(0u, x); };
-        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(
+        auto pre0 = [&]() { issue(0u, x); };           // U 16-byte loads
+        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0, decltype(pre0), U>(
             R, raw, stride, lane < gn, now, g, key != nullptr, K, E2SAR_REAS_LOOKUP_FIRST ? &pre0 : nullptr);
         L.info[lane] = cl.info;
         old = cl.old;

@@ -749,9 +749,17 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
 struct NoPre {
     __device__ void operator()() const {}
 };
+// Record tag (fused kernel): record B's valid word carries (epoch << 2) | 1 for records its
+// creators publish, so a pass-0 record read -- issued beside the claim, not after it -- is
+// trusted only when it carries this epoch's tag: a line of an earlier epoch that some path
+// still serves (the read is not ordered after the claim, whose atomic drops this XCD's L2
+// copy) never passes for a current record.  Any other valid word (1: a creator of another
+// launch form; an earlier epoch) sends the lane to a fresh read after its claim returned.
+__device__ __forceinline__ uint32_t record_tag(uint32_t epoch) { return (epoch << 2) | 1u; }
+
 template <int kPreLoads, typename Pre>
 __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
-                                           uint64_t now, const Pre &pre)
+                                           uint64_t now, const Pre &pre, uint32_t tag)
 {
     LookupResult res{kNoSlot, 0, kNoBuf};
     const uint32_t mask = R.tableSlots - 1u;
@@ -790,17 +798,17 @@ __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t
             u32x4 A, B;
             if (first) {
 #if E2SAR_REAS_READ_FIRST
-                if (A0.x == kEmpty) {
-                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-                } else {
+                if (B0.w == tag) {
                     old = kBusy;
                     A = A0;
                     B = B0;
                     haveAB = true;
+                } else {
+                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
                 }
 #else
                 old = old0;
-                if (old != kEmpty) {
+                if (old != kEmpty && B0.w == tag) {
                     A = A0;
                     B = B0;
                     haveAB = true;
@@ -823,7 +831,7 @@ __device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t
                     atomicOr(&R.ctl->errorFlags, 2u);
                 }
                 st_agent(&sl->created, now);
-                st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, 1u});
+                st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, tag});
                 st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
                 atomicAdd(occ_in_progress(R, h), 1ull);
                 atomicAdd(occ_table_used(R, h), 1ull);
@@ -1014,7 +1022,7 @@ struct Classified {
 template <bool DeferAcc = false, typename Pre = NoPre, int kPreLoads = 0>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
                                     uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{},
-                                    const Pre *pre = nullptr)
+                                    const Pre *pre = nullptr, uint32_t tag = 0u)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
@@ -1070,7 +1078,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     {
         // a caller's pre-issue hook (the fused kernel's round-0 loads) goes after the first
         // table operation; otherwise the plain lookup
-        const LookupResult lk = pre ? find_or_create_pre<kPreLoads>(R, head && !prek, ev, d, blen, now, *pre)
+        const LookupResult lk = pre ? find_or_create_pre<kPreLoads>(R, head && !prek, ev, d, blen, now, *pre, tag)
                                     : find_or_create(R, head && !prek, ev, d, blen, now);
         if (!prek) lr = lk;
     }
@@ -1341,7 +1349,9 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     GroupKeys K{};
     if (key) K = *key;
     TRACE_AT(0, 0, trace_now());
-    // every wave issues the (cached) header loads so no load result crosses a branch
+    // every wave issues the (cached) header loads so no load result crosses a branch; the
+    // table epoch (a scalar load) rides beside them
+    const uint32_t epoch = E2SAR_REAS_LOOKUP_FIRST ? R.ctl->epoch : 0u;
     const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
     TRACE_WAIT();
     TRACE_AT(2, 0, trace_now());
@@ -1402,7 +1412,8 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     if (w0) {
         auto pre0 = [&]() { issue(0u, x); };           // U 16-byte loads
         const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0, decltype(pre0), U>(
-            R, raw, stride, lane < gn, now, g, key != nullptr, K, E2SAR_REAS_LOOKUP_FIRST ? &pre0 : nullptr);
+            R, raw, stride, lane < gn, now, g, key != nullptr, K, E2SAR_REAS_LOOKUP_FIRST ? &pre0 : nullptr,
+            record_tag(epoch));
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -2316,6 +2327,7 @@ __global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dro
         R.ctl->arenaTop = 0;
         R.ctl->tableUsed = 0;
         R.ctl->inProgress = 0;
+        R.ctl->epoch = R.ctl->epoch + 1u;          // records of earlier epochs no longer match a tag
         if (dropCompleted) R.ctl->nCompleted = 0;
     }
     if (s < kShards) {
@@ -2380,6 +2392,7 @@ __global__ void reas_compact_finish(ReasDev to)
     for (uint32_t k = 0; k < kShards; k++) *occ_table_used(to, k) = 0ull;
     to.ctl->compactTop = 0;
     to.ctl->compactUsed = 0;
+    to.ctl->epoch = to.ctl->epoch + 1u;            // a new table: earlier records never match a tag
 }
 
 // ---------------------------------------------------------------------------------

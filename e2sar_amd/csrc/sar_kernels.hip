@@ -54,12 +54,6 @@ constexpr int kBlock = 256;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
-#ifndef E2SAR_REAS_LOOKUP_FIRST
-#define E2SAR_REAS_LOOKUP_FIRST 1   // reas_kernel: wave 0's first table operation before its round-0 loads
-#endif
-#ifndef E2SAR_REAS_READ_FIRST
-#define E2SAR_REAS_READ_FIRST 0     // find_or_create A/B: first pass reads records A/B (one uncontended
-#endif                              // load) and claims only a slot it finds EMPTY; 0 = claim first
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -616,9 +610,6 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
     uint32_t pass = 0;
 #endif
     bool claimed = false;          // the current slot is known to be past EMPTY: poll by loads
-#if E2SAR_REAS_READ_FIRST
-    bool peeked = false;           // records A/B of this slot were read once: EMPTY -> claim now
-#endif
     while (__ballot(active)) {
         bool waiting = false, advance = false;
         if (active) {
@@ -626,26 +617,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             // a slot never returns to EMPTY within an arena epoch, so once a claim has
             // failed, later passes poll records A/B with loads instead of repeating the CAS
             // (A/B: +1.1 % at 1 MiB / MTU 1500, +1.8 % at 8 MiB / MTU 9000)
-#if E2SAR_REAS_READ_FIRST
-            // read first: a lookup of an event that exists costs one load, not a contended CAS
-            uint32_t old;
-            u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
-            bool haveAB = false;
-            if (!claimed && !peeked) {
-                ld_slot_ab(sl, A0, B0);
-                peeked = true;
-                if (A0.x == kEmpty) {
-                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-                } else {
-                    old = kBusy;              // examined below from the records just read
-                    haveAB = true;
-                }
-            } else {
-                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-            }
-#else
             const uint32_t old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-#endif
 #if E2SAR_TRACE
             if (pass == 0) {
                 TRACE_WAIT();
@@ -677,16 +649,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             } else if (old == kBusy || old == kReady) {
                 u32x4 A, B;
-#if E2SAR_REAS_READ_FIRST
-                if (haveAB) {
-                    A = A0;
-                    B = B0;
-                } else {
-                    ld_slot_ab(sl, A, B);
-                }
-#else
                 ld_slot_ab(sl, A, B);
-#endif
                 if (A.x == kReady && B.w != 0u) {
                     if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
                         res.slot = h;
@@ -707,9 +670,6 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             }
             if (advance) {
                 claimed = false;
-#if E2SAR_REAS_READ_FIRST
-                peeked = false;
-#endif
                 h = (h + 1u) & mask;
                 if (++probes >= R.tableSlots) {
                     atomicOr(&R.ctl->errorFlags, 1u);
@@ -721,158 +681,6 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             }
         }
-        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
-#if E2SAR_TRACE
-        pass++;
-#endif
-    }
-#if E2SAR_TRACE
-    if (__ballot(want)) {
-        TRACE_FIRST(2, 2, trace_now());
-        TRACE_FIRST(2, 3, pass);
-    }
-#endif
-    return res;
-}
-
-// The fused kernel's lookup (reas_range): the same protocol as find_or_create, with the
-// first table operation of every wanting lane (the claim and a read of records A/B, or with
-// E2SAR_REAS_READ_FIRST the read only) issued BEFORE `pre` -- the caller's round-0 payload
-// loads, kPreLoads 16-byte loads issued by the whole wave -- so that waiting for it does not
-// wait for those loads too (vmcnt retires in issue order).  The pass-0 record read is the
-// same sc1 global load as ld_slot_ab, in inline asm, waited for by a counted vmcnt that
-// leaves the caller's loads in flight (the guide's asm form (ii): the wait names both
-// destinations "+v").  (Compiler-counted sc1 buffer loads for the records were tried first:
-// with them, lookups in the bench's full batch spun for seconds and an event went missing;
-// the asm global loads the protocol has always used do not.)  Later passes poll with
-// ld_slot_ab.
-struct NoPre {
-    __device__ void operator()() const {}
-};
-// Record tag (fused kernel): record B's valid word carries (epoch << 2) | 1 for records its
-// creators publish, so a pass-0 record read -- issued beside the claim, not after it -- is
-// trusted only when it carries this epoch's tag: a line of an earlier epoch that some path
-// still serves (the read is not ordered after the claim, whose atomic drops this XCD's L2
-// copy) never passes for a current record.  Any other valid word (1: a creator of another
-// launch form; an earlier epoch) sends the lane to a fresh read after its claim returned.
-__device__ __forceinline__ uint32_t record_tag(uint32_t epoch) { return (epoch << 2) | 1u; }
-
-template <int kPreLoads, typename Pre>
-__device__ LookupResult find_or_create_pre(const ReasDev &R, bool want, uint64_t ev, uint32_t d, uint32_t blen,
-                                           uint64_t now, const Pre &pre, uint32_t tag)
-{
-    LookupResult res{kNoSlot, 0, kNoBuf};
-    const uint32_t mask = R.tableSlots - 1u;
-    uint32_t h = slot_hash(ev, d, mask);
-    uint32_t probes = 0, spins = 0;
-    bool active = want;
-#if E2SAR_TRACE
-    uint32_t pass = 0;
-#endif
-    bool claimed = false;
-    // ---- the first table operation, then the caller's loads ----
-    // claim-first: the claim and a read of records A/B go out together, so a lane that finds
-    // the event already published resolves in this one round trip; read-first: the read only
-    uint32_t old0 = kBusy;
-    u32x4 A0{0u, 0u, 0u, 0u}, B0{0u, 0u, 0u, 0u};
-    if (active) {
-#if !E2SAR_REAS_READ_FIRST
-        old0 = atomicCAS(&R.slots[h].state, (uint32_t)kEmpty, (uint32_t)kBusy);
-#endif
-        asm volatile("global_load_dwordx4 %0, %2, off sc1\n\t"
-                     "global_load_dwordx4 %1, %2, off offset:16 sc1"
-                     : "=&v"(A0), "=&v"(B0)
-                     : "v"(R.slots + h)
-                     : "memory");
-    }
-    pre();
-    // the two record loads are older than the caller's kPreLoads loads: vmcnt(kPreLoads) has them
-    asm volatile("s_waitcnt vmcnt(%2)" : "+v"(A0), "+v"(B0) : "n"(kPreLoads) : "memory");
-    bool first = true;
-    while (__ballot(active)) {
-        bool waiting = false, advance = false;
-        if (active) {
-            ReasSlot *sl = R.slots + h;
-            uint32_t old;
-            bool haveAB = false;
-            u32x4 A, B;
-            if (first) {
-#if E2SAR_REAS_READ_FIRST
-                if (B0.w == tag) {
-                    old = kBusy;
-                    A = A0;
-                    B = B0;
-                    haveAB = true;
-                } else {
-                    old = atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-                }
-#else
-                old = old0;
-                if (old != kEmpty && B0.w == tag) {
-                    A = A0;
-                    B = B0;
-                    haveAB = true;
-                }
-#endif
-            } else {
-                old = claimed ? (uint32_t)kBusy : atomicCAS(&sl->state, (uint32_t)kEmpty, (uint32_t)kBusy);
-            }
-#if E2SAR_TRACE
-            if (pass == 0) {
-                TRACE_WAIT();
-                TRACE_FIRST(2, 1, trace_now());
-            }
-#endif
-            if (old == kEmpty) {
-                const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
-                uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
-                if (boff + blen > R.arenaBytes) {
-                    boff = kNoBuf;
-                    atomicOr(&R.ctl->errorFlags, 2u);
-                }
-                st_agent(&sl->created, now);
-                st16_agent(&sl->bufOff, u32x4{(uint32_t)boff, (uint32_t)(boff >> 32), blen, tag});
-                st16_agent(sl, u32x4{(uint32_t)kReady, d, (uint32_t)ev, (uint32_t)(ev >> 32)});
-                atomicAdd(occ_in_progress(R, h), 1ull);
-                atomicAdd(occ_table_used(R, h), 1ull);
-                res.slot = h;
-                res.bytes = blen;
-                res.bufOff = boff;
-                active = false;
-            } else if (old == kBusy || old == kReady) {
-                if (!haveAB) ld_slot_ab(sl, A, B);
-                if (A.x == kReady && B.w != 0u) {
-                    if (A.y == d && (((uint64_t)A.w << 32) | A.z) == ev) {
-                        res.slot = h;
-                        res.bytes = B.z;
-                        res.bufOff = ((uint64_t)B.y << 32) | B.x;
-                        active = false;
-                    } else {
-                        advance = true;
-                    }
-                } else if (A.x == kDone || A.x == kLost) {
-                    advance = true;
-                } else {
-                    waiting = true;
-                    claimed = true;
-                }
-            } else {
-                advance = true;
-            }
-            if (advance) {
-                claimed = false;
-                h = (h + 1u) & mask;
-                if (++probes >= R.tableSlots) {
-                    atomicOr(&R.ctl->errorFlags, 1u);
-                    active = false;
-                }
-            }
-            if (waiting && ++spins > kSpinLimit) {
-                atomicOr(&R.ctl->errorFlags, 4u);
-                active = false;
-            }
-        }
-        first = false;
         if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
 #if E2SAR_TRACE
         pass++;
@@ -1019,10 +827,9 @@ struct Classified {
 // per-event atomics are per run, not per datagram.
 // DeferAcc: the run tail's add to the event's accumulator is left to the caller (the fused
 // kernel issues it after its copy, so the copy's waits never sit behind that atomic).
-template <bool DeferAcc = false, typename Pre = NoPre, int kPreLoads = 0>
+template <bool DeferAcc = false>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
-                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{},
-                                    const Pre *pre = nullptr, uint32_t tag = 0u)
+                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{})
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
@@ -1065,22 +872,19 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
 
     // keys resolved by the group-key pre-pass (reas_keys_kernel): a run head whose key is
     // one of them takes its slot and buffer from the record instead of the table
-    bool prek = false;
+    bool pre = false;
     LookupResult lr{kNoSlot, 0, kNoBuf};
     if (hasKeys) {
 #pragma unroll
         for (int k = 0; k < 2; k++)
-            if (!prek && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
-                prek = true;
+            if (!pre && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
+                pre = true;
                 lr = LookupResult{K.slot[k], K.bytes[k], K.boff[k]};
             }
     }
     {
-        // a caller's pre-issue hook (the fused kernel's round-0 loads) goes after the first
-        // table operation; otherwise the plain lookup
-        const LookupResult lk = pre ? find_or_create_pre<kPreLoads>(R, head && !prek, ev, d, blen, now, *pre, tag)
-                                    : find_or_create(R, head && !prek, ev, d, blen, now);
-        if (!prek) lr = lk;
+        const LookupResult lk = find_or_create(R, head && !pre, ev, d, blen, now);
+        if (!pre) lr = lk;
     }
 
     const uint64_t H = __ballot(head);
@@ -1349,9 +1153,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     GroupKeys K{};
     if (key) K = *key;
     TRACE_AT(0, 0, trace_now());
-    // every wave issues the (cached) header loads so no load result crosses a branch; the
-    // table epoch (a scalar load) rides beside them
-    const uint32_t epoch = E2SAR_REAS_LOOKUP_FIRST ? R.ctl->epoch : 0u;
+    // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
     TRACE_WAIT();
     TRACE_AT(2, 0, trace_now());
@@ -1403,17 +1205,11 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
-    // round 0 is in flight while wave 0 classifies; wave 0 issues its own share right after
-    // its first table operation (E2SAR_REAS_LOOKUP_FIRST), so that operation's round trip is
-    // not queued behind the payload loads in vmcnt order
-    if (!(E2SAR_REAS_LOOKUP_FIRST && w0)) issue(0u, x);
+    issue(0u, x);                      // round 0 is in flight while wave 0 classifies
 
     unsigned long long old = 0;
     if (w0) {
-        auto pre0 = [&]() { issue(0u, x); };           // U 16-byte loads
-        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0, decltype(pre0), U>(
-            R, raw, stride, lane < gn, now, g, key != nullptr, K, E2SAR_REAS_LOOKUP_FIRST ? &pre0 : nullptr,
-            record_tag(epoch));
+        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(R, raw, stride, lane < gn, now, g, key != nullptr, K);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -2327,7 +2123,6 @@ __global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dro
         R.ctl->arenaTop = 0;
         R.ctl->tableUsed = 0;
         R.ctl->inProgress = 0;
-        R.ctl->epoch = R.ctl->epoch + 1u;          // records of earlier epochs no longer match a tag
         if (dropCompleted) R.ctl->nCompleted = 0;
     }
     if (s < kShards) {
@@ -2392,7 +2187,6 @@ __global__ void reas_compact_finish(ReasDev to)
     for (uint32_t k = 0; k < kShards; k++) *occ_table_used(to, k) = 0ull;
     to.ctl->compactTop = 0;
     to.ctl->compactUsed = 0;
-    to.ctl->epoch = to.ctl->epoch + 1u;            // a new table: earlier records never match a tag
 }
 
 // ---------------------------------------------------------------------------------

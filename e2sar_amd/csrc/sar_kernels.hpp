@@ -52,7 +52,7 @@ struct ReasCtl {
     uint32_t errorFlags;
     unsigned long long compactTop;   // arena top of the destination arena during compaction
     uint32_t compactUsed;            // slots claimed in the destination table
-    uint32_t epoch;                  // table epoch: +1 per recycle (the fused kernel's record tag)
+    uint32_t pad0;
     uint64_t pad[2];
     uint64_t pad2[6];
 };

@@ -294,6 +294,55 @@ __global__ __launch_bounds__(256) void dg_all(const uint8_t *slots, uint8_t *dst
     for (int k = 0; k < R * 4; k++) dg_store(dst, pg, dg_split(k * 256 + threadIdx.x, nch), x[k]);
 }
 
+// dg_pipe<49> plus the fused kernel's non-copy parts, one at a time (MODE bits):
+//   1: wave 0 writes every datagram's destination to LDS, barrier, stores read it from LDS
+//   2: wave 0 waits SLEEP_US (s_memrealtime) before that barrier -- a classification's
+//      latency -- with round 0's loads in flight
+//   4: each run tail (here: lane 0 of wave 0) issues a returning atomic add on its event's
+//      counter (event = datagram / 731) before round 1's loads; its result is used last
+struct MockLds {
+    uint64_t dst[64];
+};
+template <int G, int MODE>
+__global__ __launch_bounds__(256) void dg_mock(const uint8_t *slots, uint8_t *dst, uint32_t n,
+                                               unsigned long long *ctr, uint32_t sleepTicks)
+{
+    __shared__ MockLds L;
+    const uint32_t pg = blockIdx.x * G;
+    const uint32_t gn = (n - pg < G) ? n - pg : G;
+    const uint32_t nch = gn * kSpc;
+    const uint8_t *s = slots + (uint64_t)pg * kStride;
+    u32x4 x[4], y[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) x[u] = dg_load(s, pg, dg_split(u * 256 + threadIdx.x, nch));
+    unsigned long long old = 0;
+    if (threadIdx.x < 64) {
+        if (MODE & 2) {
+            const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+            while (__builtin_amdgcn_s_memrealtime() - t0 < sleepTicks) __builtin_amdgcn_s_sleep(8);
+        }
+        if ((MODE & 4) && threadIdx.x == 0) old = atomicAdd(ctr + (pg / 731u) * 16u, 1ull);
+        if (MODE & 1) L.dst[threadIdx.x] = (uint64_t)(dst) + (uint64_t)(pg + threadIdx.x) * kPl;
+    }
+    if (MODE & 3) __syncthreads();
+    for (uint32_t r0 = 0; r0 < nch; r0 += 1024) {
+        if (r0 + 1024 < nch) {
+#pragma unroll
+            for (int u = 0; u < 4; u++) y[u] = dg_load(s, pg, dg_split(r0 + 1024 + u * 256 + threadIdx.x, nch));
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const DgChunk d = dg_split(r0 + u * 256 + threadIdx.x, nch);
+            uint8_t *D = dst;
+            if (MODE & 1) D = reinterpret_cast<uint8_t *>(L.dst[d.p]) - (uint64_t)(pg + d.p) * kPl;
+            dg_store(D, pg, d, x[u]);
+        }
+#pragma unroll
+        for (int u = 0; u < 4; u++) x[u] = y[u];
+    }
+    if ((MODE & 4) && threadIdx.x == 0 && old == ~0ull) ctr[1] = 1;      // consume the result
+}
+
 __global__ __launch_bounds__(256) void wk_slots(const uint8_t *src, uint8_t *slots, uint32_t n)
 {
     // seg-shaped writer: 8-KiB pieces of the slot array from a random source
@@ -362,6 +411,9 @@ int main(int argc, char **argv)
     const uint32_t n = 146165;
     uint8_t *slots;
     CHECK(hipMalloc(&slots, (uint64_t)n * kStride + 4096));
+    unsigned long long *ctr;
+    CHECK(hipMalloc(&ctr, 1 << 20));
+    CHECK(hipMemset(ctr, 0, 1 << 20));
     auto timedg = [&](auto launch) {
         std::vector<float> v;
         for (int i = 0; i < iters; i++) {
@@ -393,6 +445,11 @@ int main(int argc, char **argv)
         printf(", \"naive32\": %.2f", timedg([&] { dg_naive<32><<<NG(32), 256>>>(slots, dst, n); }));
         printf(", \"rows44\": %.2f", timedg([&] { dg_rows<44><<<NG(44), 256>>>(slots, dst, n); }));
         printf(", \"rows22\": %.2f", timedg([&] { dg_rows<22><<<NG(22), 256>>>(slots, dst, n); }));
+        printf(", \"mock_lds\": %.2f", timedg([&] { dg_mock<49, 1><<<NG(49), 256>>>(slots, dst, n, ctr, 0); }));
+        printf(", \"mock_sleep3\": %.2f", timedg([&] { dg_mock<49, 3><<<NG(49), 256>>>(slots, dst, n, ctr, 300); }));
+        printf(", \"mock_sleep7\": %.2f", timedg([&] { dg_mock<49, 3><<<NG(49), 256>>>(slots, dst, n, ctr, 700); }));
+        printf(", \"mock_atomic\": %.2f", timedg([&] { dg_mock<49, 4><<<NG(49), 256>>>(slots, dst, n, ctr, 0); }));
+        printf(", \"mock_all7\": %.2f", timedg([&] { dg_mock<49, 7><<<NG(49), 256>>>(slots, dst, n, ctr, 700); }));
         // the fused kernel's residency (6 workgroups per CU): 24 KiB of dynamic LDS each
         printf(", \"one8_occ6\": %.2f", timedg([&] { dg_naive<8><<<NG(8), 256, 24576>>>(slots, dst, n); }));
         printf(", \"pipe49_occ6\": %.2f", timedg([&] { dg_pipe<49><<<NG(49), 256, 24576>>>(slots, dst, n); }));

@@ -1205,7 +1205,13 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
-    issue(0u, x);                      // round 0 is in flight while wave 0 classifies
+#ifndef E2SAR_REAS_HEAD_QUIET
+#define E2SAR_REAS_HEAD_QUIET 0
+#endif
+    // A/B: groups below E2SAR_REAS_HEAD_QUIET (the first residency wave) classify before
+    // their round-0 loads, so their claims do not queue behind the whole wave's loads
+    const bool quiet = g < (uint32_t)E2SAR_REAS_HEAD_QUIET;
+    if (!quiet) issue(0u, x);          // round 0 is in flight while wave 0 classifies
 
     unsigned long long old = 0;
     if (w0) {
@@ -1223,6 +1229,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
         TRACE_AT(0, 1, trace_now());
     }
     lds_barrier();
+    if (quiet) issue(0u, x);
     TRACE_AT(0, 2, trace_hwid());
 
 #if E2SAR_REAS_PIPE

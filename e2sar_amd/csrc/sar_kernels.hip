@@ -1205,13 +1205,10 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #if E2SAR_REAS_PIPE
     u32x4 y[U];
 #endif
-#ifndef E2SAR_REAS_HEAD_QUIET
-#define E2SAR_REAS_HEAD_QUIET 0
-#endif
-    // A/B: groups below E2SAR_REAS_HEAD_QUIET (the first residency wave) classify before
-    // their round-0 loads, so their claims do not queue behind the whole wave's loads
-    const bool quiet = g < (uint32_t)E2SAR_REAS_HEAD_QUIET;
-    if (!quiet) issue(0u, x);          // round 0 is in flight while wave 0 classifies
+    // round 0 is in flight while wave 0 classifies.  (A/B, round 4: the first residency
+    // wave's groups classifying before their round-0 loads, so their claims do not queue
+    // behind 25 MB of loads, ran 0.5-2 us slower: DESIGN 4.5.)
+    issue(0u, x);
 
     unsigned long long old = 0;
     if (w0) {
@@ -1229,7 +1226,6 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
         TRACE_AT(0, 1, trace_now());
     }
     lds_barrier();
-    if (quiet) issue(0u, x);
     TRACE_AT(0, 2, trace_hwid());
 
 #if E2SAR_REAS_PIPE

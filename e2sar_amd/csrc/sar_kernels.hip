@@ -1470,10 +1470,11 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
     }
 }
 
-// Scatter stores: 1 = destination-aligned (shift_store: source-aligned loads, the next
-// chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 2 = the same with
-// every lane loading its chunk pair itself; 0 = source-aligned chunks stored at their
-// misaligned destination (scatter_chunk), the round-2 form.
+// Scatter stores (A/B build knob): 1 = destination-aligned (shift_store: source-aligned
+// loads, the next chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 2 =
+// the same with every lane loading its chunk pair itself; 0 (default) = source-aligned
+// chunks, staged through LDS into aligned stores (lds_stage_store) where scatter_stage()
+// picks it, else stored at their misaligned destination (scatter_chunk).
 #ifndef E2SAR_SCATTER_SHIFT
 #define E2SAR_SCATTER_SHIFT 0
 #endif
@@ -1530,8 +1531,8 @@ __device__ __forceinline__ void shift_store(const PktInfo pi, uint32_t c, u32x4 
     if (h4 < hi && h4 >= l4) store_bytes(D, o, h4, hi);
 }
 
-// E2SAR_SCATTER_SHIFT == 3 (A/B): the one-round group's source-aligned chunks go through
-// LDS.  Every dword of a payload is written to its destination phase in the group's LDS
+// Staged scatter (STAGE, chosen per launch by scatter_stage()): the one-round group's
+// source-aligned chunks go through LDS.  Every dword of a payload is written to its destination phase in the group's LDS
 // copy of the slot (datagram p at p * (stride + 16), payload byte t at a + t, a = dst mod
 // 16), then after an LDS barrier every 16-byte event block is read back aligned and stored
 // aligned: the loads need nothing from the work records, the stores are whole aligned
@@ -1541,7 +1542,8 @@ template <int U>
 __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x4 (&x)[U], const uint32_t (&pp)[U],
                                                 const uint32_t (&cc)[U], uint32_t nch, uint32_t gn, uint32_t stride)
 {
-    __shared__ uint32_t stage[(16384u + 64u * 16u) / 4u];
+    // one round of the group's slots (<= 256 * U chunks) plus 16 bytes of phase per datagram
+    __shared__ uint32_t stage[(16u * kBlock * U + 64u * 16u) / 4u];
     const uint32_t ps = stride + 16u;                                  // LDS bytes per datagram
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1588,7 +1590,7 @@ __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x
 }
 
 // One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
-template <int U, bool NT>
+template <int U, bool NT, bool STAGE>
 __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                               uint32_t n, uint32_t G, const PktInfo *__restrict__ info,
                                               const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
@@ -1643,12 +1645,12 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     }
     __syncthreads();
 
-#if E2SAR_SCATTER_SHIFT == 3
-    if (nch <= (uint32_t)(kBlock * U)) {
-        lds_stage_store<U>(sinfo, x, pp, cc, nch, gn, stride);
-        nch = 0;                                                     // done: skip the rounds below
+    if constexpr (STAGE) {
+        if (nch <= (uint32_t)(kBlock * U)) {
+            lds_stage_store<U>(sinfo, x, pp, cc, nch, gn, stride);
+            nch = 0;                                                 // done: skip the rounds below
+        }
     }
-#endif
     for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
         if (r0) issue(r0);
 #pragma unroll
@@ -1762,7 +1764,7 @@ __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const 
     classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-template <int U, bool NT>
+template <int U, bool NT, bool STAGE>
 __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t n, uint32_t G,
                                                               const PktInfo *__restrict__ info,
@@ -1770,13 +1772,13 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const u
 {
     __shared__ PktInfo sinfo[64];
     if (G == 0u) scatter_range<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
-    else scatter_group<U, NT>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+    else scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
 // The classify workgroups have the low indices so they are dispatched first and their
 // round trips start while the scatter workgroups fill the machine.
-template <int U, bool NT>
+template <int U, bool NT, bool STAGE>
 __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
     const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
@@ -1793,7 +1795,7 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
     if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
-    else scatter_group<U, NT>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
+    else scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2567,6 +2569,22 @@ hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t 
     return hipGetLastError();
 }
 
+// Staged stores (scatter_group<..., STAGE>: a one-round group's chunks pass through LDS so
+// every event store is a whole aligned 16-byte store) per launch.  Measured per user,
+// interleaved on one box (profiles/round4/ab/scatter_stores_*.log): config 3's split scatter
+// (MTU 9000, streaming) 232.0-232.3 vs 235.9-236.4 us; cold leg at MTU 9000 83.4 vs 84.9-86.4
+// us; hot split scatter at MTU 1500 67.3-67.5 vs 68.5-68.7 us; reference-order batches
+// 123.0-123.6 vs 125.2-125.4 us; but the cold leg at MTU 1500 (8-datagram groups read from
+// HBM, where the LDS barrier waits for the slowest of the group's loads) 84.9-85.5 vs
+// 83.0-83.3 us.  So: staged unless the datagrams stream in at small strides.
+#ifndef E2SAR_SCATTER_STAGE
+#define E2SAR_SCATTER_STAGE 1       // A/B: 0 = never stage
+#endif
+static bool scatter_stage(uint32_t stride, bool nt)
+{
+    return E2SAR_SCATTER_STAGE && E2SAR_SCATTER_SHIFT == 0 && (!nt || stride > 2048u);
+}
+
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
                                const void *work, hipStream_t stream, bool nt)
 {
@@ -2575,12 +2593,15 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const uint8_t *w = static_cast<const uint8_t *>(work);
     uint32_t blocks = 0;
     const uint32_t G = scatter_geometry(stride, n, blocks);
-    if (nt)
-        hipLaunchKernelGGL((reas_scatter_kernel<U, true>), dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
-                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
-    else
-        hipLaunchKernelGGL((reas_scatter_kernel<U, false>), dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G,
-                           reinterpret_cast<const PktInfo *>(w), reinterpret_cast<const FinishRec *>(w + work_fin_off(n)));
+    const PktInfo *info = reinterpret_cast<const PktInfo *>(w);
+    const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G, info,
+                           fin);
+    };
+    const bool st = scatter_stage(stride, nt);
+    if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
+    else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
     return hipGetLastError();
 }
 
@@ -2603,16 +2624,16 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     // (cold leg, 205 x 1 MiB: 81.4-83.8 vs 83.9-87.0 us per launch over three boxes, 50 / 65 /
     // 80 / 88 % in between; profiles/round3/s3_cls/)
     const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * E2SAR_PIPE_CLS_AT / 100u);
-    if (nt)
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, true>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
-                       spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
-                       reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
-                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls, clsStart);
-    else
-    hipLaunchKernelGGL((reas_scatter_classify_kernel<U, false>), dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride,
-                       spk, sn, G, reinterpret_cast<const PktInfo *>(sw),
-                       reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
-                       reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls, clsStart);
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride, spk, sn, G,
+                           reinterpret_cast<const PktInfo *>(sw),
+                           reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
+                           reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,
+                           clsStart);
+    };
+    const bool st = scatter_stage(stride, nt);
+    if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
+    else st ? go(reas_scatter_classify_kernel<U, false, true>) : go(reas_scatter_classify_kernel<U, false, false>);
     return hipGetLastError();
 }
 

@@ -1538,21 +1538,12 @@ __device__ __forceinline__ void shift_store(const PktInfo pi, uint32_t c, u32x4 
 // aligned: the loads need nothing from the work records, the stores are whole aligned
 // 16-byte stores except at the payload's two edges.  A payload that is not dword-congruent
 // with its destination (never at dword-multiple maxPld) is stored from registers as before.
-// The staging buffer, one per kernel for both staged forms: one round of slots (256 * U
-// chunks) plus 16 bytes of phase per datagram of a group (<= 64) or 32 per datagram of a
-// range (<= kStageSlots).
-template <int U>
-__device__ __forceinline__ uint32_t *stage_lds()
-{
-    __shared__ uint32_t stage[(16u * kBlock * U + 64u * 16u) / 4u];
-    return stage;
-}
-
 template <int U>
 __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x4 (&x)[U], const uint32_t (&pp)[U],
                                                 const uint32_t (&cc)[U], uint32_t nch, uint32_t gn, uint32_t stride)
 {
-    uint32_t *const stage = stage_lds<U>();
+    // one round of the group's slots (<= 256 * U chunks) plus 16 bytes of phase per datagram
+    __shared__ uint32_t stage[(16u * kBlock * U + 64u * 16u) / 4u];
     const uint32_t ps = stride + 16u;                                  // LDS bytes per datagram
 #pragma unroll
     for (int u = 0; u < U; u++) {
@@ -1765,135 +1756,6 @@ __device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *_
     }
 }
 
-// Staged form of scatter_range (E2SAR_SCATTER_RANGE == 2 with staging): the range's loads
-// are the linear 16-KiB copy of scatter_range, and every payload dword goes through LDS to
-// its destination phase, as in lds_stage_store, so the event stores are whole aligned 16-byte
-// stores.  Datagram j of the range owns an LDS region of the aligned event blocks its bytes
-// in this range touch; a block a range boundary cuts is written partially (dword stores) by
-// each of the two ranges, each with only its own bytes.  At most kStageSlots datagrams may
-// touch one range (host-checked).
-constexpr uint32_t kStageSlots = 16;
-template <int U, bool NT>
-__device__ __forceinline__ void scatter_range_staged(const ReasDev &R, const uint8_t *__restrict__ pkts,
-                                                     uint32_t stride, uint32_t n, const PktInfo *__restrict__ info,
-                                                     const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
-{
-    constexpr uint32_t K = (uint32_t)kBlock * U;
-    static_assert(32u * kStageSlots <= 64u * 16u, "range staging fits the shared buffer");
-    uint32_t *const stage = stage_lds<U>();
-    __shared__ uint32_t sreg[kStageSlots + 1], sb0[kStageSlots], slo[kStageSlots], shi[kStageSlots];
-    const uint32_t spc = stride >> 4;
-    const uint64_t total = (uint64_t)n * spc;
-    const uint64_t c0 = (uint64_t)blk * K;
-    const uint32_t nch = (total - c0 < K) ? (uint32_t)(total - c0) : K;
-    const uint32_t p0 = (uint32_t)(c0 / spc);
-    const uint32_t ns = (uint32_t)((c0 + nch - 1u) / spc) - p0 + 1u;   // <= kStageSlots (host-checked)
-    const uint32_t skew = (uint32_t)(c0 - (uint64_t)p0 * spc);
-    const uint32_t lane = threadIdx.x & 63u;
-    const PktInfo mine = ld_info(info + p0 + ((lane < ns) ? lane : 0u));
-
-    const float rspc = 1.0f / (float)spc;
-    const uint8_t *const base = pkts + 16ull * c0;
-    u32x4 x[U];
-    uint32_t pp[U], cc[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
-        const uint32_t rc = (r < nch) ? r : 0u;
-        const uint32_t l = skew + rc;
-        uint32_t p = (uint32_t)((float)l * rspc);
-        if (p * spc > l) p--;
-        else if ((p + 1u) * spc <= l) p++;
-        pp[u] = p;
-        cc[u] = l - p * spc;
-        x[u] = NT ? ld16_nt(base + 16u * rc) : ld16(base + 16u * rc);
-    }
-    bool fins = false;
-    if (threadIdx.x < 64) {
-        const uint64_t lo = (uint64_t)R.arena, hi = lo + R.arenaBytes;
-        const bool inside = mine.plen == 0 || (mine.dst >= lo && mine.dst + mine.plen <= hi);
-        const bool own = lane < ns && (lane > 0u || skew == 0u);
-        if (own && !inside) atomicOr(&R.ctl->errorFlags, 8u);
-        PktInfo v = (lane < ns && inside) ? mine : PktInfo{0ull, 0u, 0u};
-        fins = own && (v.hl & kPktCompletes) != 0u;
-        v.hl &= ~kPktCompletes;
-        // this range's bytes of datagram `lane`: chunks [cs, ce) of it, payload slot bytes
-        // [s0, s1), aligned event blocks [b0, b0 + nb) relative to dst & ~15
-        uint32_t nb = 0, b0 = 0, bl = 0, bh = 0;
-        const uint32_t a = (uint32_t)v.dst & 15u;
-        if (lane < ns && v.plen != 0u && ((a - v.hl) & 3u) == 0u) {
-            const uint32_t cs = (lane == 0u) ? skew : 0u;
-            const uint32_t ce = (skew + nch - lane * spc < spc) ? skew + nch - lane * spc : spc;
-            const uint32_t s0 = (16u * cs > v.hl) ? 16u * cs : v.hl;
-            const uint32_t s1 = (16u * ce < v.hl + v.plen) ? 16u * ce : v.hl + v.plen;
-            if (s0 < s1) {
-                bl = a + s0 - v.hl;                                       // event-phase byte range
-                bh = a + s1 - v.hl;
-                b0 = bl >> 4;
-                nb = ((bh - 1u) >> 4) - b0 + 1u;
-            }
-        }
-        const uint32_t inc = wave_incl_scan(nb);
-        if (lane < ns) {
-            sreg[lane] = inc - nb;
-            sb0[lane] = b0;
-            slo[lane] = bl;
-            shi[lane] = bh;
-        }
-        if (lane == ns - 1u) sreg[ns] = inc;
-        sinfo[lane] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
-        if (r >= nch) continue;
-        const uint32_t j = pp[u];
-        const PktInfo pi = sinfo[j];
-        if (pi.plen == 0u) continue;
-        const uint32_t a = (uint32_t)pi.dst & 15u;
-        if (((a - pi.hl) & 3u) != 0u) {                                   // not dword-congruent
-            scatter_chunk(pi, cc[u], x[u]);
-            continue;
-        }
-        // payload slot byte s lands at LDS byte 16 (sreg - sb0) + a + s - hl
-        const uint32_t off = 16u * (sreg[j] - sb0[j]) + a - pi.hl;
-#pragma unroll
-        for (uint32_t d = 0; d < 4; d++) {
-            const uint32_t sb = 16u * cc[u] + 4u * d;
-            if (sb >= pi.hl && sb < pi.hl + pi.plen) stage[(off + sb) >> 2] = x[u][d];
-        }
-    }
-    lds_barrier();
-    const uint32_t nbt = sreg[ns];
-    for (uint32_t k = threadIdx.x; k < nbt; k += kBlock) {
-        uint32_t j = 0;
-        while (j + 1u < ns && sreg[j + 1u] <= k) j++;
-        const PktInfo pi = sinfo[j];
-        const uint32_t b = sb0[j] + (k - sreg[j]);
-        const u32x4 o{stage[4u * k], stage[4u * k + 1u], stage[4u * k + 2u], stage[4u * k + 3u]};
-        uint8_t *D = reinterpret_cast<uint8_t *>((pi.dst & ~15ull) + 16ull * b);
-        const uint32_t bl = slo[j], bh = shi[j];
-        const uint32_t lo = (16u * b < bl) ? bl - 16u * b : 0u;
-        const uint32_t hi = (16u * b + 16u > bh) ? bh - 16u * b : 16u;
-        if (lo == 0u && hi == 16u) {
-            st16_nt(D, o);
-            continue;
-        }
-#pragma unroll
-        for (uint32_t d = 0; d < 4; d++)
-            if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
-        const uint32_t t = hi & ~3u;                                       // sub-dword event tail
-        if (t < hi && t >= lo) store_bytes(D, o, t, hi);
-    }
-    if (fins) {
-        const FinishRec f = fin[p0 + lane];
-        const uint32_t fs = f.slot & ~kFinKeepSlot;
-        if (fs < R.tableSlots) complete_event(R, fs, f.ev, f.boff, f.bytes, f.d, f.frags, (f.slot & kFinKeepSlot) != 0u);
-        else atomicOr(&R.ctl->errorFlags, 8u);
-    }
-}
-
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,
                                                                uint32_t n, uint64_t now, PktInfo *__restrict__ info,
@@ -1909,12 +1771,8 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const u
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    if (G == 0u) {
-        if constexpr (STAGE) scatter_range_staged<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
-        else scatter_range<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
-    } else {
-        scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
-    }
+    if (G == 0u) scatter_range<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
+    else scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
@@ -1936,12 +1794,8 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
         return;
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
-    if (G == 0u) {
-        if constexpr (STAGE) scatter_range_staged<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
-        else scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
-    } else {
-        scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
-    }
+    if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
+    else scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2564,14 +2418,11 @@ static_assert(E2SAR_PIPE_CLS_AT >= 0 && E2SAR_PIPE_CLS_AT <= 100, "percent");
 // most kRangeSlots datagrams can touch one range, else groups of G whole datagrams.
 // Returns G (0 = ranges) and the workgroup count.
 static uint32_t scatter_group_size(uint32_t stride);
-static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks, bool stage)
+static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
 {
     constexpr uint32_t K = (uint32_t)kBlock * E2SAR_SCATTER_U;
     const uint32_t spc = stride >> 4;
-    // 1: ranges always; 2: ranges where the launch stages its stores (scatter_range_staged)
-    const uint32_t slots = (E2SAR_SCATTER_RANGE == 2) ? (stage ? kStageSlots : 0u)
-                         : (E2SAR_SCATTER_RANGE == 1 && !stage) ? kRangeSlots : 0u;
-    if (slots && !E2SAR_SCATTER_G && spc && (K + spc - 2u) / spc + 1u <= slots) {
+    if (E2SAR_SCATTER_RANGE && !E2SAR_SCATTER_G && spc && (K + spc - 2u) / spc + 1u <= kRangeSlots) {
         blocks = (uint32_t)(((uint64_t)n * spc + K - 1u) / K);
         return 0u;
     }
@@ -2741,14 +2592,14 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     uint32_t blocks = 0;
-    const bool st = scatter_stage(stride, nt);
-    const uint32_t G = scatter_geometry(stride, n, blocks, st);
+    const uint32_t G = scatter_geometry(stride, n, blocks);
     const PktInfo *info = reinterpret_cast<const PktInfo *>(w);
     const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G, info,
                            fin);
     };
+    const bool st = scatter_stage(stride, nt);
     if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
     else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
     return hipGetLastError();
@@ -2764,8 +2615,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     const uint8_t *sw = static_cast<const uint8_t *>(swork);
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     uint32_t sblocks = 0;
-    const bool st = scatter_stage(stride, nt);
-    const uint32_t G = scatter_geometry(stride, sn, sblocks, st);
+    const uint32_t G = scatter_geometry(stride, sn, sblocks);
     const uint32_t nCls = cdiv(cn, kBlock);
     // where the classify workgroups sit in the grid: E2SAR_PIPE_CLS_AT percent of the way
     // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
@@ -2781,6 +2631,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                            reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,
                            clsStart);
     };
+    const bool st = scatter_stage(stride, nt);
     if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
     else st ? go(reas_scatter_classify_kernel<U, false, true>) : go(reas_scatter_classify_kernel<U, false, false>);
     return hipGetLastError();

@@ -86,6 +86,8 @@ def parse(argv=None):
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
+    ap.add_argument("--reas-group", type=int, default=0,
+                    help="A/B: datagrams per fused-reassembly workgroup (1..64; 0 = the library's balanced choice)")
     ap.add_argument("--table-factor", type=int, default=8,
                     help="event-table slots = next power of two >= factor x events per step")
     ap.add_argument("--cold-steps", type=int, default=10,
@@ -457,7 +459,8 @@ def run_workload(args, env, headline: bool):
     from e2sar_amd import _capi
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
-                              flags=_capi.REAS_REFERENCE_ORDER if args.reference_order else 0)
+                              flags=_capi.REAS_REFERENCE_ORDER if args.reference_order else 0,
+                              group_size=args.reas_group)
     if args.landing == "spread":
         R.set_owner(world, rank)          # reassemble only this rank's events (eventNum % world)
     if args.reference_order and args.reas != "fused":

@@ -26,6 +26,13 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
+#ifndef E2SAR_SCATTER_THREADS
+#define E2SAR_SCATTER_THREADS 256   // scatter (and pipelined scatter+classify) workgroup size (A/B knob)
+#endif
+constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
+#ifndef E2SAR_REAS_THREADS
+#define E2SAR_REAS_THREADS 0        // reas_kernel workgroup size: 0 = by stride (768, or 512 for jumbo slots); A/B knob
+#endif
 #ifndef E2SAR_REAS_POLL_SLEEP
 #define E2SAR_REAS_POLL_SLEEP 1       // s_sleep units (64 clocks) between slot polls
 #endif
@@ -1139,7 +1146,7 @@ struct ReasGroupLds {
 //   5. the run tails complete events (their atomic results are consumed last).
 // HO: the chained form -- every datagram byte and length is read with sc1 loads (they were
 // stored write-through by seg_block in the same launch).
-template <int U, bool HO = false>
+template <int U, bool HO = false, int NT = kBlock>
 __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t g0, uint32_t gn, uint64_t now,
                                            uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ key)
@@ -1182,7 +1189,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     auto issue = [&](uint32_t r0, u32x4(&xs)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kBlock + tx;
+            const uint32_t i = r0 + (uint32_t)u * NT + tx;
             uint32_t p, c;
             split_chunk(i, p, c);
             const uint32_t a = __shfl(gPhase, (int)p), plen = __shfl(gPlen, (int)p);
@@ -1194,7 +1201,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     auto store = [&](uint32_t r0, const u32x4(&xs)[U]) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kBlock + tx;
+            const uint32_t i = r0 + (uint32_t)u * NT + tx;
             if (i >= nch) continue;
             uint32_t p, c;
             split_chunk(i, p, c);
@@ -1233,7 +1240,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
     // a store can only be waited for together with that store's write acknowledgement;
     // issued before it, round r+1's data is waited for while round r's stores drain.
-    constexpr uint32_t RS = (uint32_t)(kBlock * U);
+    constexpr uint32_t RS = (uint32_t)(NT * U);
     if (RS < nch) issue(RS, y);
     store(0u, x);
     for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
@@ -1245,7 +1252,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     }
 #else
     store(0u, x);
-    for (uint32_t r0 = (uint32_t)(kBlock * U); r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+    for (uint32_t r0 = (uint32_t)(NT * U); r0 < nch; r0 += (uint32_t)(NT * U)) {
         issue(r0, x);
         store(r0, x);
     }
@@ -1279,7 +1286,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 
 // starts (optional): group g is datagrams [starts[g], starts[g+1]) (<= 64), e.g. the XCD
 // stripes of the batch's segmentation (seg_groups); otherwise [g*G, g*G + G).
-template <int U, bool HO = false>
+template <int U, bool HO = false, int NT = kBlock>
 __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
                                            uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr,
@@ -1295,7 +1302,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
         if (g1 <= g0 || g1 - g0 > 64u) return;                       // empty or oversized group
         gn = g1 - g0;
     }
-    reas_range<U, HO>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
+    reas_range<U, HO, NT>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
 }
 
 // reas_kernel: workgroup b reassembles datagrams [b*G, b*G + G) of the batch.
@@ -1307,15 +1314,28 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 // classifier wave that classifies the next group while copy waves copy the current one,
 // then an LDS ring of classified groups: bit-exact, 79.7-81.8 us against 74-75 us here --
 // the groups buffered per workgroup when the queues run dry lengthen the tail)
-template <int U>
-__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
-                                                                           uint32_t stride, const uint32_t *__restrict__ lens,
-                                                                           uint32_t n, uint64_t now, uint32_t G,
-                                                                           const GroupKeys *__restrict__ keys,
-                                                                           const uint32_t *__restrict__ starts)
+// NT threads per workgroup: wave 0 classifies while all NT/64 waves hold a round of loads
+// (NT x U chunks) in flight.  Round 4 (profiles/round4/ab/reas_threads.log,
+// reas_group_sizes.log): 768 threads (two workgroups of 12 waves per CU, 59-datagram
+// groups in 1.8 rounds) take the 1 MiB @ MTU 1500 batch in 72.7-72.9 us against 75.4-75.7
+// at 256 (six of 4 waves, 49 datagrams in 4.4 rounds); with jumbo slots 512 threads do
+// best (71.0 against 73.4-74.0 us at 256 and 71.7 at 768); 1024 threads (one workgroup
+// per CU) lose (82-84 us).
+template <int U, int NT>
+__global__ __launch_bounds__(NT) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+                                                                   uint32_t stride, const uint32_t *__restrict__ lens,
+                                                                   uint32_t n, uint64_t now, uint32_t G,
+                                                                   const GroupKeys *__restrict__ keys,
+                                                                   const uint32_t *__restrict__ starts)
 {
     __shared__ ReasGroupLds L;
-    reas_group<U>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys, starts);
+    reas_group<U, false, NT>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys, starts);
+}
+
+// reas_kernel's workgroup size for a slot stride
+__host__ __device__ constexpr int reas_threads(uint32_t stride)
+{
+    return E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : (stride <= 4096u ? 768 : 512);
 }
 
 // Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
@@ -1543,11 +1563,11 @@ __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x
                                                 const uint32_t (&cc)[U], uint32_t nch, uint32_t gn, uint32_t stride)
 {
     // one round of the group's slots (<= 256 * U chunks) plus 16 bytes of phase per datagram
-    __shared__ uint32_t stage[(16u * kBlock * U + 64u * 16u) / 4u];
+    __shared__ uint32_t stage[(16u * kScatBlock * U + 64u * 16u) / 4u];
     const uint32_t ps = stride + 16u;                                  // LDS bytes per datagram
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t i = (uint32_t)u * kBlock + threadIdx.x;
+        const uint32_t i = (uint32_t)u * kScatBlock + threadIdx.x;
         if (i >= nch) continue;
         const PktInfo pi = sinfo[pp[u]];
         if (pi.plen == 0u) continue;
@@ -1566,7 +1586,7 @@ __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x
     lds_barrier();
     const uint32_t nbp = ps >> 4;                                      // 16-byte blocks per datagram
     const uint32_t total = gn * nbp;
-    for (uint32_t k = threadIdx.x; k < total; k += kBlock) {
+    for (uint32_t k = threadIdx.x; k < total; k += kScatBlock) {
         const uint32_t p = k / nbp, b = k - p * nbp;
         const PktInfo pi = sinfo[p];
         if (pi.plen == 0u) continue;
@@ -1616,7 +1636,7 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     auto issue = [&](uint32_t r0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            const uint32_t i = r0 + (uint32_t)u * kScatBlock + threadIdx.x;
             const uint32_t ic = (i < nch) ? i : 0u;
             uint32_t p = (uint32_t)((float)ic * rspc);
             if (p * spc > ic) p--;
@@ -1646,17 +1666,17 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     __syncthreads();
 
     if constexpr (STAGE) {
-        if (nch <= (uint32_t)(kBlock * U)) {
+        if (nch <= (uint32_t)(kScatBlock * U)) {
             lds_stage_store<U>(sinfo, x, pp, cc, nch, gn, stride);
             nch = 0;                                                 // done: skip the rounds below
         }
     }
-    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kBlock * U)) {
+    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kScatBlock * U)) {
         if (r0) issue(r0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
             // next chunk from lane + 1 (whole wave active: DPP reads every lane)
-            const uint32_t i = r0 + (uint32_t)u * kBlock + threadIdx.x;
+            const uint32_t i = r0 + (uint32_t)u * kScatBlock + threadIdx.x;
 #if E2SAR_SCATTER_SHIFT == 2
             if (i >= nch) continue;
             shift_store(sinfo[pp[u]], cc[u], x[u], xn[u]);          // every lane loaded its pair
@@ -1703,7 +1723,7 @@ __device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *_
                                               uint32_t n, const PktInfo *__restrict__ info,
                                               const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
 {
-    constexpr uint32_t K = (uint32_t)kBlock * U;
+    constexpr uint32_t K = (uint32_t)kScatBlock * U;
     const uint32_t spc = stride >> 4;
     const uint64_t total = (uint64_t)n * spc;
     const uint64_t c0 = (uint64_t)blk * K;
@@ -1720,7 +1740,7 @@ __device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *_
     uint32_t pp[U], cc[U];
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
+        const uint32_t r = (uint32_t)u * kScatBlock + threadIdx.x;
         const uint32_t rc = (r < nch) ? r : 0u;
         const uint32_t l = skew + rc;                                     // chunk index from datagram p0's start
         uint32_t p = (uint32_t)((float)l * rspc);
@@ -1744,7 +1764,7 @@ __device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *_
     __syncthreads();
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kBlock + threadIdx.x;
+        const uint32_t r = (uint32_t)u * kScatBlock + threadIdx.x;
         if (r >= nch) continue;
         scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
     }
@@ -1765,7 +1785,7 @@ __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const 
 }
 
 template <int U, bool NT, bool STAGE>
-__global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+__global__ __launch_bounds__(kScatBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t n, uint32_t G,
                                                               const PktInfo *__restrict__ info,
                                                               const FinishRec *__restrict__ fin)
@@ -1779,7 +1799,7 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_kernel(ReasDev R, const u
 // The classify workgroups have the low indices so they are dispatched first and their
 // round trips start while the scatter workgroups fill the machine.
 template <int U, bool NT, bool STAGE>
-__global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
+__global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
     const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
     const uint32_t *__restrict__ clens, uint32_t cn, uint64_t now, PktInfo *__restrict__ cinfo,
@@ -1790,7 +1810,7 @@ __global__ __launch_bounds__(kBlock) void reas_scatter_classify_kernel(
     const uint32_t b = blockIdx.x;
     if (b - clsStart < nClsBlocks) {
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
-                              (b - clsStart) * (kBlock / 64) + (threadIdx.x >> 6));
+                              (b - clsStart) * (kScatBlock / 64) + (threadIdx.x >> 6));
         return;
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
@@ -2232,7 +2252,7 @@ static_assert(E2SAR_SCATTER_G <= 64 && E2SAR_SCATTER_LDS <= 65536 && E2SAR_PIPE_
 #define E2SAR_SEG_STRIPE 1          // seg_kernel writes XCD stripes (seg_groups); 0 = linear units (A/B knob)
 #endif
 
-template <int U>
+template <int U, int NT>
 static uint32_t reas_resident_groups();
 
 // Geometry of seg_kernel for a batch: 16-byte chunks per thread, units per event and the
@@ -2261,7 +2281,7 @@ static bool seg_geom(uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t str
     const uint32_t target = std::min<uint32_t>(49u, std::max<uint32_t>(1u, E2SAR_REAS_CHUNKS_PER_BLOCK / spc));
     const uint32_t S0 = std::max<uint32_t>(1u, (uint32_t)((uint64_t)target * spc / g.unitChunks));
     uint32_t best = S0;
-    const uint32_t cap = reas_resident_groups<E2SAR_REAS_U>();
+    const uint32_t cap = reas_resident_groups<E2SAR_REAS_U, kBlock>();
     if (cap && g.nUnits) {
         const uint64_t waves = ((g.nUnits + S0 - 1) / S0 + cap - 1) / cap;
         uint32_t bestDev = ~0u;
@@ -2420,7 +2440,7 @@ static_assert(E2SAR_PIPE_CLS_AT >= 0 && E2SAR_PIPE_CLS_AT <= 100, "percent");
 static uint32_t scatter_group_size(uint32_t stride);
 static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
 {
-    constexpr uint32_t K = (uint32_t)kBlock * E2SAR_SCATTER_U;
+    constexpr uint32_t K = (uint32_t)kScatBlock * E2SAR_SCATTER_U;
     const uint32_t spc = stride >> 4;
     if (E2SAR_SCATTER_RANGE && !E2SAR_SCATTER_G && spc && (K + spc - 2u) / spc + 1u <= kRangeSlots) {
         blocks = (uint32_t)(((uint64_t)n * spc + K - 1u) / K);
@@ -2440,13 +2460,13 @@ static uint32_t scatter_group_size(uint32_t stride)
     // fused kernel's 9K budget (89.5 us at 2K); hot, 68.7 us.
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK) G >>= 1;
+    while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK * (kScatBlock / kBlock)) G >>= 1;
     return E2SAR_SCATTER_G ? (uint32_t)E2SAR_SCATTER_G : G;   // build knob: exact datagrams per workgroup
 }
 
 
-// Workgroups of reas_kernel<U> the current device holds at once (0 if unknown), per device.
-template <int U>
+// Workgroups of reas_kernel<U, NT> the current device holds at once (0 if unknown), per device.
+template <int U, int NT>
 static uint32_t reas_resident_groups()
 {
     static std::atomic<uint32_t> cache[64];
@@ -2455,7 +2475,7 @@ static uint32_t reas_resident_groups()
     uint32_t c = cache[dev].load(std::memory_order_relaxed);
     if (c) return c;
     int per = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U>, kBlock, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U, NT>, NT, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0 || cus <= 0)
         return 0;
     c = (uint32_t)per * (uint32_t)cus;
@@ -2464,7 +2484,7 @@ static uint32_t reas_resident_groups()
 }
 
 // fixedG: the reassembler's configured group size (e2sar_hip_reas_config.groupSize), 0 = auto
-static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG)
+static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG, int NT)
 {
     if (fixedG) return fixedG < 64u ? fixedG : 64u;
     constexpr int U = E2SAR_REAS_U;
@@ -2484,7 +2504,8 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG)
     // 9 % at G 16 -> 10). 205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
     // reas_kernel 79.0 -> 77.6 us.
     if (E2SAR_REAS_BALANCE) {
-        const uint32_t cap = reas_resident_groups<U>();
+        const uint32_t cap = NT == 768 ? reas_resident_groups<U, 768>()
+                           : NT == 512 ? reas_resident_groups<U, 512>() : reas_resident_groups<U, kBlock>();
         if (cap) {
             const uint32_t G0 = G, waves = cdiv(cdiv(n, G0), cap);
             uint32_t best = G0, bestDev = ~0u;
@@ -2502,7 +2523,7 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG)
 
 uint32_t reas_launch_groups(const ReasDev &R, uint32_t n, uint32_t stride)
 {
-    return n ? cdiv(n, reas_group_size(n, stride, R.groupSize)) : 0u;
+    return n ? cdiv(n, reas_group_size(n, stride, R.groupSize, reas_threads(stride))) : 0u;
 }
 
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
@@ -2510,15 +2531,23 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0) return hipSuccess;
-    const uint32_t G = reas_group_size(n, stride, R.groupSize);
+    const int NT = reas_threads(stride);
+    const uint32_t G = reas_group_size(n, stride, R.groupSize, NT);
     const uint32_t groups = cdiv(n, G);
     if (keys) {
         const uint32_t waves = cdiv(groups, 32u);
         hipLaunchKernelGGL(reas_keys_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, pkts, stride,
                            lens, n, now, G, groups, keys);
     }
-    hipLaunchKernelGGL((reas_kernel<U>), dim3(groups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, G,
-                       (const GroupKeys *)keys, (const uint32_t *)nullptr);
+    if (NT == 768)
+        hipLaunchKernelGGL((reas_kernel<U, 768>), dim3(groups), dim3(768), 0, stream, R, pkts, stride, lens, n, now, G,
+                           (const GroupKeys *)keys, (const uint32_t *)nullptr);
+    else if (NT == 512)
+        hipLaunchKernelGGL((reas_kernel<U, 512>), dim3(groups), dim3(512), 0, stream, R, pkts, stride, lens, n, now, G,
+                           (const GroupKeys *)keys, (const uint32_t *)nullptr);
+    else
+        hipLaunchKernelGGL((reas_kernel<U, kBlock>), dim3(groups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
+                           now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 
@@ -2529,7 +2558,7 @@ hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint3
 {
     constexpr int U = E2SAR_REAS_U;
     if (n == 0 || nGroups == 0) return hipSuccess;
-    hipLaunchKernelGGL((reas_kernel<U>), dim3(nGroups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, 64u,
+    hipLaunchKernelGGL((reas_kernel<U, kBlock>), dim3(nGroups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, 64u,
                        (const GroupKeys *)nullptr, starts);
     return hipGetLastError();
 }
@@ -2545,7 +2574,7 @@ hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint3
         const uint64_t chunks = (uint64_t)B.maxPacketsPerEvent * (stride >> 4);
         if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
         B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * E2SAR_CHAIN_SEG_U) : 0u;
-        B.G = B.n ? reas_group_size(B.n, stride, R.groupSize) : 1u;
+        B.G = B.n ? reas_group_size(B.n, stride, R.groupSize, kBlock) : 1u;
         B.start = (uint32_t)grid;
         B.nSeg = B.bpe * B.nEvents;
         grid += (uint64_t)B.nSeg + (B.n ? cdiv(B.n, B.G) : 0u);
@@ -2596,7 +2625,7 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const PktInfo *info = reinterpret_cast<const PktInfo *>(w);
     const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G, info,
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G, info,
                            fin);
     };
     const bool st = scatter_stage(stride, nt);
@@ -2616,7 +2645,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     uint32_t sblocks = 0;
     const uint32_t G = scatter_geometry(stride, sn, sblocks);
-    const uint32_t nCls = cdiv(cn, kBlock);
+    const uint32_t nCls = cdiv(cn, kScatBlock);
     // where the classify workgroups sit in the grid: E2SAR_PIPE_CLS_AT percent of the way
     // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
     // workgroup slots through their dependent round trips while the scatter ramps up; three
@@ -2625,7 +2654,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     // 80 / 88 % in between; profiles/round3/s3_cls/)
     const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * E2SAR_PIPE_CLS_AT / 100u);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kBlock), E2SAR_PIPE_LDS, stream, R, stride, spk, sn, G,
+        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), E2SAR_PIPE_LDS, stream, R, stride, spk, sn, G,
                            reinterpret_cast<const PktInfo *>(sw),
                            reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                            reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,

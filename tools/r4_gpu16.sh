@@ -16,3 +16,5 @@ run c3 "--mtu 9000 --event-bytes 8388608 --events 280 --batch-events 70" base s5
 run cold9000 "--mtu 9000 --cold-steps 10" base s512 s512g3
 run cold1500 "--cold-steps 10" base s512
 run split "--reas split" base s512
+run stripe "" base stripe0
+run stripe9k "--mtu 9000" base stripe0

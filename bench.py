@@ -866,6 +866,11 @@ def run_workload(args, env, headline: bool):
                          "all_launch_ms": {k: round(sum(v) / len(v), 5) for k, v in cper.items()}},
             "flags": "E2SAR_HIP_REAS_COLD_DATAGRAMS",
         }
+        ctr, csrc = _pmc_traffic(args, ckern)
+        cold["roofline"]["traffic"] = ctr
+        if ctr is not None:
+            cold["roofline"]["traffic_unit"] = "bytes per launch (rocprofv3 PMC, committed)"
+            cold["roofline"]["traffic_source"] = csrc
         del cbufs
         R.close()
         R = R_hot

@@ -33,7 +33,8 @@ for w in sorted(os.listdir(prof)) if os.path.isdir(prof) else []:
         d = json.load(open(pmc))
         d["file"] = os.path.relpath(pmc, root)
         json.dump(d, open(pmc, "w"), indent=1)
-        name = {"headline": "pmc_latest.json", "mtu9000": "pmc_mtu9000.json", "config3": "pmc_config3.json"}.get(w)
+        name = {"headline": "pmc_latest.json", "mtu9000": "pmc_mtu9000.json", "config3": "pmc_config3.json",
+                "cold": "pmc_cold.json"}.get(w)
         if name:
             json.dump(d, open(os.path.join(root, "profiles", name), "w"), indent=1)
 c3 = os.path.join(src, "c3")

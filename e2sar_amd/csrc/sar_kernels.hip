@@ -61,6 +61,9 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_EARLY
+#define E2SAR_REAS_EARLY 0          // reas_kernel: rounds 0 and 1 in flight during classification (A/B)
+#endif
 #ifndef E2SAR_REAS_DEFER_ACC
 #define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
 #endif                               // add to the event accumulator after the copy (0: never)
@@ -1216,6 +1219,12 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     // wave's groups classifying before their round-0 loads, so their claims do not queue
     // behind 25 MB of loads, ran 0.5-2 us slower: DESIGN 4.5.)
     issue(0u, x);
+#if E2SAR_REAS_PIPE && E2SAR_REAS_EARLY
+    // round 1 too (its registers exist for the software pipeline anyway): with 768-thread
+    // workgroups rounds 0 and 1 are the whole group
+    constexpr uint32_t RS0 = (uint32_t)(NT * U);
+    if (RS0 < nch) issue(RS0, y);
+#endif
 
     unsigned long long old = 0;
     if (w0) {
@@ -1241,7 +1250,9 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     // a store can only be waited for together with that store's write acknowledgement;
     // issued before it, round r+1's data is waited for while round r's stores drain.
     constexpr uint32_t RS = (uint32_t)(NT * U);
+#if !E2SAR_REAS_EARLY
     if (RS < nch) issue(RS, y);
+#endif
     store(0u, x);
     for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
         if (r0 + RS < nch) issue(r0 + RS, x);
@@ -1333,9 +1344,11 @@ __global__ __launch_bounds__(NT) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev 
 }
 
 // reas_kernel's workgroup size for a slot stride
+constexpr int kReasNTSmall = E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : 768;   // slots of <= 4 KiB
+constexpr int kReasNTJumbo = E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : 512;
 __host__ __device__ constexpr int reas_threads(uint32_t stride)
 {
-    return E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : (stride <= 4096u ? 768 : 512);
+    return stride <= 4096u ? kReasNTSmall : kReasNTJumbo;
 }
 
 // Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
@@ -2504,8 +2517,9 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG, in
     // 9 % at G 16 -> 10). 205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
     // reas_kernel 79.0 -> 77.6 us.
     if (E2SAR_REAS_BALANCE) {
-        const uint32_t cap = NT == 768 ? reas_resident_groups<U, 768>()
-                           : NT == 512 ? reas_resident_groups<U, 512>() : reas_resident_groups<U, kBlock>();
+        const uint32_t cap = NT == kReasNTSmall ? reas_resident_groups<U, kReasNTSmall>()
+                           : NT == kReasNTJumbo ? reas_resident_groups<U, kReasNTJumbo>()
+                                                : reas_resident_groups<U, kBlock>();
         if (cap) {
             const uint32_t G0 = G, waves = cdiv(cdiv(n, G0), cap);
             uint32_t best = G0, bestDev = ~0u;
@@ -2539,15 +2553,12 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
         hipLaunchKernelGGL(reas_keys_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, pkts, stride,
                            lens, n, now, G, groups, keys);
     }
-    if (NT == 768)
-        hipLaunchKernelGGL((reas_kernel<U, 768>), dim3(groups), dim3(768), 0, stream, R, pkts, stride, lens, n, now, G,
-                           (const GroupKeys *)keys, (const uint32_t *)nullptr);
-    else if (NT == 512)
-        hipLaunchKernelGGL((reas_kernel<U, 512>), dim3(groups), dim3(512), 0, stream, R, pkts, stride, lens, n, now, G,
-                           (const GroupKeys *)keys, (const uint32_t *)nullptr);
+    if (stride <= 4096u)
+        hipLaunchKernelGGL((reas_kernel<U, kReasNTSmall>), dim3(groups), dim3(kReasNTSmall), 0, stream, R, pkts, stride,
+                           lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
     else
-        hipLaunchKernelGGL((reas_kernel<U, kBlock>), dim3(groups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n,
-                           now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
+        hipLaunchKernelGGL((reas_kernel<U, kReasNTJumbo>), dim3(groups), dim3(kReasNTJumbo), 0, stream, R, pkts, stride,
+                           lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 

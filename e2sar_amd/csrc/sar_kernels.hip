@@ -61,6 +61,9 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_PROBE_NOAR
+#define E2SAR_PROBE_NOAR 0
+#endif
 #ifndef E2SAR_REAS_EARLY
 #define E2SAR_REAS_EARLY 0          // reas_kernel: rounds 0 and 1 in flight during classification (A/B)
 #endif
@@ -643,7 +646,11 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             } else if (old == kEmpty) {
                 // this lane owns the slot: buffer, then records B and A
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
+#if E2SAR_PROBE_NOAR     // probe build only (not an allocator): offsets from the event number
+                uint64_t boff = (ev % 1024ull) * (need ? need : 256ull);
+#else
                 uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
+#endif
                 if (boff + blen > R.arenaBytes) {
                     boff = kNoBuf;
                     atomicOr(&R.ctl->errorFlags, 2u);

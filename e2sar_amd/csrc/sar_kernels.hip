@@ -61,8 +61,8 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
-#ifndef E2SAR_REAS_PRIO
-#define E2SAR_REAS_PRIO 0           // reas_kernel: wave priority of the classifier during classification (A/B)
+#ifndef E2SAR_PIPE_CLS_PRIO
+#define E2SAR_PIPE_CLS_PRIO 0       // pipelined scatter+classify: wave priority of the classify waves (A/B)
 #endif
 #ifndef E2SAR_PROBE_NOAR
 #define E2SAR_PROBE_NOAR 0
@@ -1238,13 +1238,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 
     unsigned long long old = 0;
     if (w0) {
-#if E2SAR_REAS_PRIO
-        __builtin_amdgcn_s_setprio(E2SAR_REAS_PRIO);     // the classifier's chain issues first on its SIMD
-#endif
         const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(R, raw, stride, lane < gn, now, g, key != nullptr, K);
-#if E2SAR_REAS_PRIO
-        __builtin_amdgcn_s_setprio(0);
-#endif
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -1838,6 +1832,9 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     // workgroups [clsStart, clsStart + nClsBlocks) classify, the others scatter in order
     const uint32_t b = blockIdx.x;
     if (b - clsStart < nClsBlocks) {
+#if E2SAR_PIPE_CLS_PRIO
+        __builtin_amdgcn_s_setprio(E2SAR_PIPE_CLS_PRIO);
+#endif
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
                               (b - clsStart) * (kScatBlock / 64) + (threadIdx.x >> 6));
         return;

@@ -346,14 +346,19 @@ def test_reas_small_table_collisions(hip, reas_mode):
         assert len(got) == 48 and st.errorFlags == 0
 
 
-@pytest.mark.parametrize("group", [1, 7, 33, 49, 63])
-def test_reas_group_sizes(hip, group):
+@pytest.mark.parametrize("mtu,group", [(1500, g) for g in (1, 7, 33, 49, 59, 63, 64)] +
+                         [(9000, g) for g in (1, 3, 16, 64)])
+def test_reas_group_sizes(hip, mtu, group):
     # datagrams per reassembly workgroup other than the power of two the chunk budget gives
-    # (the launcher's wave balancing picks e.g. 49 at the bench's 205-event batches): groups
-    # that cut through runs, events and the float chunk split, against the oracle
+    # (the launcher's wave balancing picks e.g. 59 at the bench's 205-event batches): groups
+    # that cut through runs, events and the float chunk split, against the oracle -- with the
+    # 768-thread kernel (slots of <= 4 KiB) and the 512-thread one (jumbo slots), from part
+    # of one copy round to many
     sizes = [70000, 1, 1437, 33333, 100000, 5000, 2873]
-    evs, pk, ln = _events_stream(7, sizes, 1500, seed=101)
-    starts = np.cumsum([0] + [O.num_packets(s, O.max_pld_len(1500)) for s in sizes])[:-1].tolist()
+    if mtu == 9000:
+        sizes = [s * 4 for s in sizes]
+    evs, pk, ln = _events_stream(7, sizes, mtu, seed=101)
+    starts = np.cumsum([0] + [O.num_packets(s, O.max_pld_len(mtu)) for s in sizes])[:-1].tolist()
     rest = [i for i in range(len(ln)) if i not in starts]
     random.Random(group).shuffle(rest)
     order = starts + rest              # offset 0 first, the rest shuffled

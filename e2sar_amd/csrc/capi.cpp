@@ -109,7 +109,10 @@ static hipError_t note_launch(e2sar_hip_reas *r, hipStream_t s)
 
 // reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
 // that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
-static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
+#ifndef E2SAR_FUSED_MAX_MIB
+#define E2SAR_FUSED_MAX_MIB 320     // A/B knob
+#endif
+static constexpr uint64_t kFusedMaxBytes = (uint64_t)E2SAR_FUSED_MAX_MIB << 20;
 
 // Group-key pre-pass in front of the fused kernel (reas_keys_kernel; build knob, A/B in
 // DESIGN.md 4.5)

@@ -61,9 +61,6 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
-#ifndef E2SAR_PIPE_CLS_PRIO
-#define E2SAR_PIPE_CLS_PRIO 0       // pipelined scatter+classify: wave priority of the classify waves (A/B)
-#endif
 #ifndef E2SAR_PROBE_NOAR
 #define E2SAR_PROBE_NOAR 0
 #endif
@@ -1832,9 +1829,6 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     // workgroups [clsStart, clsStart + nClsBlocks) classify, the others scatter in order
     const uint32_t b = blockIdx.x;
     if (b - clsStart < nClsBlocks) {
-#if E2SAR_PIPE_CLS_PRIO
-        __builtin_amdgcn_s_setprio(E2SAR_PIPE_CLS_PRIO);
-#endif
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
                               (b - clsStart) * (kScatBlock / 64) + (threadIdx.x >> 6));
         return;

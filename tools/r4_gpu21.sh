@@ -14,3 +14,5 @@ print('  cold', '$f'.split('/')[-1], c['value'], c['roofline']['avg_launch_ms'],
 }
 run cold1500 "--cold-steps 10" base cp3 cp3a0 cp3a50
 run cold9000 "--mtu 9000 --cold-steps 10" base cp3 cp3a0
+tools/ab_libs.sh r4_gpu21/c3 2 "--mtu 9000 --event-bytes 8388608 --events 280 --batch-events 70" base fusedbig > $O/c3.log 2>&1 || { echo "c3 failed"; cat $O/c3.log; exit 1; }
+echo "== c3 (fused 512-thread kernel on config 3's 590 MB batches)"; cat $O/c3.log

@@ -2632,6 +2632,19 @@ static bool scatter_stage(uint32_t stride, bool nt)
     return E2SAR_SCATTER_STAGE && E2SAR_SCATTER_SHIFT == 0 && (!nt || stride > 2048u);
 }
 
+// Dynamic LDS of an unstaged streaming scatter launch (cold datagrams at small strides): an
+// occupancy cap of 6 workgroups per CU instead of 8.  Round 4, cold leg at MTU 1500
+// (profiles/round4/ab/scatter_occupancy.log): 82.7 vs 83.5-83.9 us per pipelined launch at
+// 6 per CU, 84.8-86.0 at 5, 88.0-88.8 at 4; staged launches (their own 18 KiB of LDS) lose
+// with any cap (config 3 284-286 vs 232 us at 3 per CU), so they keep none.
+#ifndef E2SAR_COLD_SCATTER_LDS
+#define E2SAR_COLD_SCATTER_LDS 24576
+#endif
+static size_t scatter_lds(bool stage, bool nt, size_t knob)
+{
+    return (!stage && nt && knob == 0) ? (size_t)E2SAR_COLD_SCATTER_LDS : knob;
+}
+
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
                                const void *work, hipStream_t stream, bool nt)
 {
@@ -2642,11 +2655,11 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const uint32_t G = scatter_geometry(stride, n, blocks);
     const PktInfo *info = reinterpret_cast<const PktInfo *>(w);
     const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
-    auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), E2SAR_SCATTER_LDS, stream, R, pkts, stride, n, G, info,
-                           fin);
-    };
     const bool st = scatter_stage(stride, nt);
+    const size_t lds = scatter_lds(st, nt, E2SAR_SCATTER_LDS);
+    auto go = [&](auto kernel) {
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), lds, stream, R, pkts, stride, n, G, info, fin);
+    };
     if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
     else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
     return hipGetLastError();
@@ -2671,14 +2684,15 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     // (cold leg, 205 x 1 MiB: 81.4-83.8 vs 83.9-87.0 us per launch over three boxes, 50 / 65 /
     // 80 / 88 % in between; profiles/round3/s3_cls/)
     const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * E2SAR_PIPE_CLS_AT / 100u);
+    const bool st = scatter_stage(stride, nt);
+    const size_t lds = scatter_lds(st, nt, E2SAR_PIPE_LDS);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), E2SAR_PIPE_LDS, stream, R, stride, spk, sn, G,
+        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), lds, stream, R, stride, spk, sn, G,
                            reinterpret_cast<const PktInfo *>(sw),
                            reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                            reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,
                            clsStart);
     };
-    const bool st = scatter_stage(stride, nt);
     if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
     else st ? go(reas_scatter_classify_kernel<U, false, true>) : go(reas_scatter_classify_kernel<U, false, false>);
     return hipGetLastError();

@@ -327,6 +327,16 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 #ifndef E2SAR_SEG_BLOCK
 #define E2SAR_SEG_BLOCK 256         // seg_kernel threads per workgroup (A/B knob)
 #endif
+#ifndef E2SAR_SEG_LDS
+#define E2SAR_SEG_LDS 0             // dynamic LDS per seg_kernel<2> workgroup: occupancy cap (A/B knob)
+#endif
+// seg_kernel<4> (16-KiB workgroups, events of more than 4 MiB of datagrams) at most 6
+// workgroups per CU: config 3's segmentation 180.0-181.4 vs 185.3 us; seg_kernel<2> loses
+// with any cap (7 / 6 / 5 per CU: 67.4-68.2 / 71.3-72.3 / 76.6-77.9 vs 67.7-70.0 us at 1 MiB;
+// profiles/round4/ab/seg_occupancy.log)
+#ifndef E2SAR_SEG_LDS4
+#define E2SAR_SEG_LDS4 24576
+#endif
 #ifndef E2SAR_SEG_STORE
 #define E2SAR_SEG_STORE 0           // datagram stores: 0 plain, 1 sc1 (write-through), 2 nt (A/B knob)
 #endif
@@ -2328,11 +2338,11 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                                     : sg.nUnits;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (sg.U == 2)
-        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, sg.bpe,
-                           lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
+        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), E2SAR_SEG_LDS, stream, d_events,
+                           sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
     else
-        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), 0, stream, d_events, sg.bpe,
-                           lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
+        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), E2SAR_SEG_LDS4, stream, d_events,
+                           sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
     return hipGetLastError();
 }
 

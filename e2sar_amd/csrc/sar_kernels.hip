@@ -61,6 +61,9 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_SMALL_LDS
+#define E2SAR_REAS_SMALL_LDS 0      // same for the small-slot (<= 4 KiB) reas_kernel launch (A/B knob)
+#endif
 #ifndef E2SAR_REAS_JUMBO_LDS
 #define E2SAR_REAS_JUMBO_LDS 0      // dynamic LDS of the jumbo-slot reas_kernel launch: occupancy cap (A/B knob)
 #endif
@@ -2574,8 +2577,8 @@ hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t str
                            lens, n, now, G, groups, keys);
     }
     if (stride <= 4096u)
-        hipLaunchKernelGGL((reas_kernel<U, kReasNTSmall>), dim3(groups), dim3(kReasNTSmall), 0, stream, R, pkts, stride,
-                           lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
+        hipLaunchKernelGGL((reas_kernel<U, kReasNTSmall>), dim3(groups), dim3(kReasNTSmall), E2SAR_REAS_SMALL_LDS, stream, R,
+                           pkts, stride, lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
     else
         hipLaunchKernelGGL((reas_kernel<U, kReasNTJumbo>), dim3(groups), dim3(kReasNTJumbo), E2SAR_REAS_JUMBO_LDS, stream, R,
                            pkts, stride, lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);

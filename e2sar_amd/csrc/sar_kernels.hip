@@ -65,7 +65,8 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #define E2SAR_REAS_SMALL_LDS 0      // same for the small-slot (<= 4 KiB) reas_kernel launch (A/B knob)
 #endif
 #ifndef E2SAR_REAS_JUMBO_LDS
-#define E2SAR_REAS_JUMBO_LDS 0      // dynamic LDS of the jumbo-slot reas_kernel launch: occupancy cap (A/B knob)
+#define E2SAR_REAS_JUMBO_LDS 56000  // dynamic LDS of the jumbo-slot reas_kernel launch: caps it at 2 workgroups
+                                    // per CU (MTU 9000: 71.2 -> 69.3 us, profiles/round4/ab/jumbo_cold_caps.log)
 #endif
 #ifndef E2SAR_PROBE_NOAR
 #define E2SAR_PROBE_NOAR 0

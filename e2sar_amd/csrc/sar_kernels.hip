@@ -61,6 +61,9 @@ constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
 #ifndef E2SAR_REAS_PIPE
 #define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
 #endif
+#ifndef E2SAR_REAS_BALANCE_LDS
+#define E2SAR_REAS_BALANCE_LDS 0
+#endif
 #ifndef E2SAR_REAS_SMALL_LDS
 #define E2SAR_REAS_SMALL_LDS 0      // same for the small-slot (<= 4 KiB) reas_kernel launch (A/B knob)
 #endif
@@ -2512,7 +2515,12 @@ static uint32_t reas_resident_groups()
     uint32_t c = cache[dev].load(std::memory_order_relaxed);
     if (c) return c;
     int per = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U, NT>, NT, 0) != hipSuccess ||
+    // E2SAR_REAS_BALANCE_LDS: balance on the occupancy the capped launch really gets (A/B knob;
+    // 0 = on the uncapped occupancy, as the caps were measured)
+    const size_t dyn = !E2SAR_REAS_BALANCE_LDS ? 0
+                     : NT == kReasNTSmall      ? (size_t)E2SAR_REAS_SMALL_LDS
+                     : NT == kReasNTJumbo      ? (size_t)E2SAR_REAS_JUMBO_LDS : 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U, NT>, NT, dyn) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0 || cus <= 0)
         return 0;
     c = (uint32_t)per * (uint32_t)cus;

@@ -736,3 +736,37 @@ def test_reas_large_events_with_loss_fused(hip, mtu, batches, group):
     ro.gc(500)
     R.gc(now_ms=1000, timeout_ms=500)
     assert sorted((r.eventNum, r.dataId, r.numFragments) for r in R.lost_poll()) == sorted(ro.lost_pop_all())
+
+
+def test_duplicate_inside_a_run_default_vs_reference_order(hip):
+    """Pins where the default device path departs from the reference under a duplicate
+    (DESIGN 5.3).  The reference tests completion after every fragment (cpp:398-403): with
+    arrival d0, d2, d3, d4 (tail), d1, d1 it meets the event's length at d1 -- the event
+    completes, whole -- and the repeated d1 opens a new item that never completes.  The
+    default device path adds per run of equal keys: the six datagrams are one run in one
+    group, whose single add (83 bytes) passes the 67-byte length without meeting it, so the
+    event stays in progress.  REFERENCE_ORDER mode gives the reference's result exactly."""
+    from e2sar_amd import _capi, sar
+    torch = _torch()
+    evs, pk, ln = _events_stream(1, len(SEND_STR), 80)
+    assert pk.shape[0] == 5
+    order = [0, 2, 3, 4, 1, 1]
+    pk, ln = pk[order], ln[order]
+    ref, rst, _ = _reas_oracle(pk, ln, True)
+    assert set(ref) == {(0, 4321)} and ref[(0, 4321)] == evs[0].tobytes()
+    assert rst["eventSuccess"] == 1 and rst["inProgress"] == 1   # the repeated d1's own item
+    got, st, _ = _reas_gpu(hip, pk, ln, True, group_size=64)
+    assert got == {} and st.eventSuccess == 0 and st.inProgress == 1
+    assert st.totalPackets == 6 and st.badHeaderDiscards == 0 and st.dataErrCnt == 0
+    # reference-order mode: the reference's events and counters
+    n, stride = pk.shape
+    dpk = _dev(pk.reshape(-1), hip)
+    dln = _dev(np.ascontiguousarray(ln, np.uint32).view(np.int32), hip)
+    R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=64, arena_bytes=1 << 20,
+                              flags=_capi.REAS_REFERENCE_ORDER)
+    R.reassemble(dpk, stride, dln, n)
+    torch.cuda.synchronize()
+    recs = R.poll()
+    assert [(r.eventNum, r.dataId) for r in recs] == [(0, 4321)]
+    assert R.event_bytes(recs[0]) == ref[(0, 4321)]
+    _check_reas({(0, 4321): (R.event_bytes(recs[0]), recs[0].numFragments)}, R.stats(), ref, rst)

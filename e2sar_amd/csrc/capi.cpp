@@ -76,8 +76,6 @@ struct e2sar_hip_reas {
         size_t roWorkBytes = 0;
         void *tiles = nullptr;
         size_t tilesBytes = 0;
-        void *keys = nullptr;            // group-key pre-pass records of the fused kernel
-        size_t keysBytes = 0;
     };
     std::map<hipStream_t, Scratch> scratch;
     std::vector<void *> retired;
@@ -109,16 +107,7 @@ static hipError_t note_launch(e2sar_hip_reas *r, hipStream_t s)
 
 // reassemble_batch keeps the fused kernel up to this many bytes of datagram slots (a batch
 // that can still sit in the 256 MiB Infinity Cache) and switches to the split form above
-#ifndef E2SAR_FUSED_MAX_MIB
-#define E2SAR_FUSED_MAX_MIB 320     // A/B knob
-#endif
-static constexpr uint64_t kFusedMaxBytes = (uint64_t)E2SAR_FUSED_MAX_MIB << 20;
-
-// Group-key pre-pass in front of the fused kernel (reas_keys_kernel; build knob, A/B in
-// DESIGN.md 4.5)
-#ifndef E2SAR_REAS_PREPASS
-#define E2SAR_REAS_PREPASS 0
-#endif
+static constexpr uint64_t kFusedMaxBytes = 320ull << 20;
 
 // Streaming (non-temporal) datagram loads in the scatter: for datagrams the caller declares
 // cold (E2SAR_HIP_REAS_COLD_DATAGRAMS), and for a batch too large to still be cached.
@@ -156,7 +145,6 @@ static void free_internal(e2sar_hip_reas *r)
         if (kv.second.roScratch) (void)hipFree(kv.second.roScratch);
         if (kv.second.roWork) (void)hipFree(kv.second.roWork);
         if (kv.second.tiles) (void)hipFree(kv.second.tiles);
-        if (kv.second.keys) (void)hipFree(kv.second.keys);
     }
     r->scratch.clear();
     for (void *p : r->retired) (void)hipFree(p);
@@ -172,7 +160,7 @@ static void drop_scratch(e2sar_hip_reas *r, hipStream_t s)
 {
     auto it = r->scratch.find(s);
     if (it == r->scratch.end()) return;
-    for (void *p : {it->second.roScratch, it->second.roWork, it->second.tiles, it->second.keys}) {
+    for (void *p : {it->second.roScratch, it->second.roWork, it->second.tiles}) {
         if (!p) continue;
         if (r->sawCapture) r->retired.push_back(p);
         else (void)hipFree(p);
@@ -247,19 +235,10 @@ int e2sar_hip_ctx_sync(e2sar_hip_ctx *ctx)
     return E2SAR_HIP_OK;
 }
 
-// A/B build knob: large device buffers (arena, e2sar_hip_device_alloc) physically contiguous
-// (hipDeviceMallocContiguous), falling back to hipMalloc when that fails
-#ifndef E2SAR_ALLOC_CONTIGUOUS
-#define E2SAR_ALLOC_CONTIGUOUS 0
-#endif
-static hipError_t dev_malloc(void **p, size_t bytes)
-{
-#if E2SAR_ALLOC_CONTIGUOUS
-    if (hipExtMallocWithFlags(p, bytes, hipDeviceMallocContiguous) == hipSuccess) return hipSuccess;
-    (void)hipGetLastError();
-#endif
-    return hipMalloc(p, bytes);
-}
+// Large device buffers (arena, e2sar_hip_device_alloc).  (Round 3: physically contiguous
+// allocations, hipDeviceMallocContiguous, made config 3's scatter 27 % slower at every
+// offset)
+static hipError_t dev_malloc(void **p, size_t bytes) { return hipMalloc(p, bytes); }
 
 int e2sar_hip_device_alloc(e2sar_hip_ctx *ctx, size_t bytes, void **out)
 {
@@ -657,13 +636,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
         if (e != hipSuccess) return hip_fail(e, "reassembly launch (split form)");
         return E2SAR_HIP_OK;
     }
-    GroupKeys *keys = nullptr;
-    if (E2SAR_REAS_PREPASS) {
-        const size_t kb = sizeof(GroupKeys) * (size_t)reas_launch_groups(r->dev, nPackets, stride);
-        if (int rc = grow(r, s, sc.keys, sc.keysBytes, kb)) return rc;
-        keys = static_cast<GroupKeys *>(sc.keys);
-    }
-    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s, keys);
+    hipError_t e = launch_reassemble(r->dev, d_packets, stride, d_lens, nPackets, now_ms, s);
     if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "reassembly launch");
     return E2SAR_HIP_OK;

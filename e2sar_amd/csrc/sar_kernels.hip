@@ -26,76 +26,22 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef u32x4 __attribute__((aligned(4))) u32x4_a4;   // 16-byte access at dword alignment
 
 constexpr int kBlock = 256;
-#ifndef E2SAR_SCATTER_THREADS
-#define E2SAR_SCATTER_THREADS 256   // scatter (and pipelined scatter+classify) workgroup size (A/B knob)
-#endif
-constexpr int kScatBlock = E2SAR_SCATTER_THREADS;
-#ifndef E2SAR_REAS_THREADS
-#define E2SAR_REAS_THREADS 0        // reas_kernel workgroup size: 0 = by stride (768, or 512 for jumbo slots); A/B knob
-#endif
-#ifndef E2SAR_REAS_POLL_SLEEP
-#define E2SAR_REAS_POLL_SLEEP 1       // s_sleep units (64 clocks) between slot polls
-#endif
-
-// Occupancy cap of the fused reassembly kernel (0 = whatever its registers allow).
-#ifndef E2SAR_REAS_WAVES
-#define E2SAR_REAS_WAVES 0
-#endif
-#if E2SAR_REAS_WAVES
-#define E2SAR_REAS_WAVES_ATTR __attribute__((amdgpu_waves_per_eu(E2SAR_REAS_WAVES, E2SAR_REAS_WAVES)))
-#else
-#define E2SAR_REAS_WAVES_ATTR
-#endif
-#ifndef E2SAR_REAS_U
-#define E2SAR_REAS_U 4
-#endif
-#ifndef E2SAR_SCATTER_U
-#define E2SAR_SCATTER_U E2SAR_REAS_U // 16-byte chunks per thread per round of the scatter forms
-#endif
-// seg_kernel's 16-byte output chunks per thread (U) is chosen per launch (launch_segment):
-// 8-KiB workgroups (U = 2) for events of up to 4 MiB of datagrams, 16-KiB (U = 4) above.
-// A/B (profiles/round2/ab2/segu*, suc3*, su9k): 205 x 1 MiB at MTU 1500, U = 2 1414-1422
-// GiB/s, 3 1414, 4 1399-1404, 6 1397, 8 1362, 1 1341; 1 MiB at MTU 9000, U = 2 1434 vs 4
-// 1418; 8 MiB at MTU 9000 (32 per launch), U = 2 1325-1334 vs 4 1362-1371.  E2SAR_SEG_U
-// (env, 2 or 4) overrides.
-#ifndef E2SAR_REAS_PIPE
-#define E2SAR_REAS_PIPE 1           // reas_kernel: loads of round r+1 issued before stores of round r
-#endif
-#ifndef E2SAR_REAS_BALANCE_LDS
-#define E2SAR_REAS_BALANCE_LDS 0
-#endif
-#ifndef E2SAR_REAS_SMALL_LDS
-#define E2SAR_REAS_SMALL_LDS 0      // same for the small-slot (<= 4 KiB) reas_kernel launch (A/B knob)
-#endif
-#ifndef E2SAR_REAS_JUMBO_LDS
-#define E2SAR_REAS_JUMBO_LDS 56000  // dynamic LDS of the jumbo-slot reas_kernel launch: caps it at 2 workgroups
-                                    // per CU (MTU 9000: 71.2 -> 69.3 us, profiles/round4/ab/jumbo_cold_caps.log)
-#endif
-#ifndef E2SAR_PROBE_NOAR
-#define E2SAR_PROBE_NOAR 0
-#endif
-#ifndef E2SAR_REAS_EARLY
-#define E2SAR_REAS_EARLY 0          // reas_kernel: rounds 0 and 1 in flight during classification (A/B)
-#endif
-#ifndef E2SAR_REAS_DEFER_ACC
-#define E2SAR_REAS_DEFER_ACC 4194304 // reas_kernel: run tails of events of at least this many bytes
-#endif                               // add to the event accumulator after the copy (0: never)
-#ifndef E2SAR_CHAIN_SEG_U
-// chained form: seg blocks of 16 KiB (8-KiB blocks, as seg_kernel uses for 1 MiB events,
-// made the chained launch 147 -> 158 us: twice the blocks at the reassembly occupancy)
-#define E2SAR_CHAIN_SEG_U 4
-#endif
+// Launch geometry, fixed at the measured best (DESIGN.md 4.5 holds every A/B behind these
+// numbers; round 5 removed the build-time switches whose alternatives lost).
+constexpr int kScatBlock = 256;             // scatter / pipelined scatter+classify workgroup
+constexpr uint32_t kPollSleep = 1;          // s_sleep units (64 clocks) between table slot polls
+constexpr int kReasU = 4;                   // 16-byte chunks per thread per copy round (fused kernel)
+constexpr int kScatU = 4;                   // the same for the scatter forms
+// fused kernel: run tails of events of at least this many bytes add to the event
+// accumulator after the copy, not during classification
+constexpr uint32_t kDeferAccBytes = 4194304u;
 // Split / pipelined scatter loads: non-temporal for datagrams that were written long before
 // (not in the Infinity Cache), plain for a batch just written -- chosen per launch
 // (launch_reas_scatter's nt; capi.cpp: E2SAR_HIP_REAS_COLD_DATAGRAMS, or a batch too large to
 // be cached).  Cold: a 205 x 1 MiB batch's scatter 85.1 (nt) vs 89.3 us (plain); hot: 68.0
 // (plain) vs 89.4 us (nt), reference-order batches 124.8 vs 148.1 us (profiles/round2/ab3/nt).
-#ifndef E2SAR_SCATTER_CHUNKS_PER_BLOCK
-#define E2SAR_SCATTER_CHUNKS_PER_BLOCK 1024u
-#endif
-#ifndef E2SAR_REAS_CHUNKS_PER_BLOCK
-#define E2SAR_REAS_CHUNKS_PER_BLOCK 9216u
-#endif
+constexpr uint32_t kScatterChunksPerBlock = 1024u;   // one round of 256 threads x 4 chunks
+constexpr uint32_t kReasChunksPerBlock = 9216u;      // fused group budget before balancing
 
 // Timeline trace (experiment builds only, -DE2SAR_TRACE=1): per workgroup, s_memrealtime
 // (100 MHz) at start, after classification, after the barrier and at the end, plus HW_ID.
@@ -144,40 +90,12 @@ __device__ __forceinline__ u32x4 ld16_nt(const uint8_t *p)
     return __builtin_nontemporal_load((const E2SAR_GLOBAL u32x4_a4 *)(p));
 }
 __device__ __forceinline__ void st16_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4 *)(p)); }
-// 16-byte store at a dword-aligned (not 16-byte-aligned) address (non-temporal unless
-// E2SAR_REAS_NT_STORE=0)
-#ifndef E2SAR_REAS_NT_STORE
-#define E2SAR_REAS_NT_STORE 1
-#endif
-__device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v)
-{
-#if E2SAR_REAS_NT_STORE == 2       // A/B: sc1 (write-through)
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#elif E2SAR_REAS_NT_STORE == 3     // A/B: sc1 nt
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#elif E2SAR_REAS_NT_STORE
-    __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4_a4 *)(p));
-#else
-    *(E2SAR_GLOBAL u32x4_a4 *)(p) = v;
-#endif
-}
+// 16-byte non-temporal store at a dword-aligned (not 16-byte-aligned) address: event
+// bytes written by the reassembly kernels.  (Round 3, profiles/round3/ab_ntstore/ and
+// s2_ab_store/: cache-allocating event stores evict the batch's datagrams from the Infinity
+// Cache -- reas_kernel 74 -> 108 us; write-through (sc1) stores 153-220 us.)
+__device__ __forceinline__ void st16u_nt(uint8_t *p, u32x4 v) { __builtin_nontemporal_store(v, (E2SAR_GLOBAL u32x4_a4 *)(p)); }
 __device__ __forceinline__ void st1(uint8_t *p, uint8_t v) { *(E2SAR_GLOBAL uint8_t *)(p) = v; }
-// Aligned 16-byte event store of the fused reassembly (A/B knob E2SAR_REAS_EV_STORE):
-// 0 nt (the line stays in the XCD's L2 until written back), 1 sc1 (write-through: the line
-// leaves L2, nothing of it is left dirty for the kernel-end write-back), 2 sc1 nt.
-#ifndef E2SAR_REAS_EV_STORE
-#define E2SAR_REAS_EV_STORE 0
-#endif
-__device__ __forceinline__ void st16_ev(uint8_t *p, u32x4 v)
-{
-#if E2SAR_REAS_EV_STORE == 1
-    asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#elif E2SAR_REAS_EV_STORE == 2
-    asm volatile("global_store_dwordx4 %0, %1, off sc1 nt\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-#else
-    st16_nt(p, v);
-#endif
-}
 
 // Agent-coherent (sc1) forms for bytes handed from one workgroup to another inside a
 // launch (the chained segment -> reassemble form): the producer stores every handed-off
@@ -215,17 +133,7 @@ __device__ __forceinline__ uint8_t ld1_sc1(const uint8_t *p)
 // Workgroup barrier that orders LDS only.  __syncthreads() also waits for every global
 // load and atomic the wave has outstanding; here a classifier's fire-and-forget counter
 // atomics and the payload loads of the other waves stay in flight across it.
-#ifndef E2SAR_REAS_LDS_BARRIER
-#define E2SAR_REAS_LDS_BARRIER 1
-#endif
-__device__ __forceinline__ void lds_barrier()
-{
-#if E2SAR_REAS_LDS_BARRIER
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-#else
-    __syncthreads();
-#endif
-}
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // ---------------------------------------------------------------------------------
 // segmentation
@@ -334,22 +242,12 @@ __device__ __forceinline__ u32x4 keep_low_bytes(u32x4 o, uint32_t n)
 // once the block's stores are done, the block adds the number of index-space chunks it
 // covered in each reassembly group's range of datagrams to that group's counter
 // (tiles[slot / tileG]); a group starts when its counter reaches its slots x stride/16.
-#ifndef E2SAR_SEG_BLOCK
-#define E2SAR_SEG_BLOCK 256         // seg_kernel threads per workgroup (A/B knob)
-#endif
-#ifndef E2SAR_SEG_LDS
-#define E2SAR_SEG_LDS 0             // dynamic LDS per seg_kernel<2> workgroup: occupancy cap (A/B knob)
-#endif
+constexpr int kSegBlock = 256;       // seg_kernel threads per workgroup (128 / 512 lost)
 // seg_kernel<4> (16-KiB workgroups, events of more than 4 MiB of datagrams) at most 6
 // workgroups per CU: config 3's segmentation 180.0-181.4 vs 185.3 us; seg_kernel<2> loses
 // with any cap (7 / 6 / 5 per CU: 67.4-68.2 / 71.3-72.3 / 76.6-77.9 vs 67.7-70.0 us at 1 MiB;
 // profiles/round4/ab/seg_occupancy.log)
-#ifndef E2SAR_SEG_LDS4
-#define E2SAR_SEG_LDS4 24576
-#endif
-#ifndef E2SAR_SEG_STORE
-#define E2SAR_SEG_STORE 0           // datagram stores: 0 plain, 1 sc1 (write-through), 2 nt (A/B knob)
-#endif
+constexpr uint32_t kSeg4PerCU = 6;
 // One round of a segmentation block: index-space chunks [j0, j0 + SB*U) of event ev,
 // bounded by jEnd (the event's chunk count, or the end of a local chained range).
 struct SegEv {
@@ -467,8 +365,9 @@ __device__ __forceinline__ void seg_round(const SegEv &E, uint8_t *__restrict__ 
         } else {
             o = u32x4{h.w0, h.w1, h.w2, h.w3};
         }
-        if (HO || E2SAR_SEG_STORE == 1) st16_sc1(outR, 16u * (jj[u] - outJ0), o);
-        else if (E2SAR_SEG_STORE == 2) st16_nt(out + 16u * jj[u], o);
+        // plain stores: the batch stays in the Infinity Cache for the reassembly that reads it
+        // next (nt stores: reas_kernel 97.8 vs 74 us, round 3)
+        if (HO) st16_sc1(outR, 16u * (jj[u] - outJ0), o);
         else st16(out + 16u * jj[u], o);
     }
 }
@@ -529,7 +428,7 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
 // the Infinity Cache.  Units are numbered e * blocksPerEvent + bx as
 // without stripes; units past nUnits exit.
 template <int U>
-__global__ __launch_bounds__(E2SAR_SEG_BLOCK) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
+__global__ __launch_bounds__(kSegBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                               uint32_t blocksPerEvent, int lbVersion,
                                                               uint32_t maxPld, uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t *__restrict__ lens,
@@ -542,7 +441,7 @@ __global__ __launch_bounds__(E2SAR_SEG_BLOCK) void seg_kernel(const e2sar_hip_se
         blk = ((k / stripe) * 8u + x) * stripe + k % stripe;
         if (blk >= nUnits) return;
     }
-    seg_block<U, false, E2SAR_SEG_BLOCK>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount,
+    seg_block<U, false, kSegBlock>(events, blocksPerEvent, lbVersion, maxPld, pkts, stride, lens, dCount,
                                          blk, 1u, nullptr);
 }
 
@@ -666,11 +565,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
             } else if (old == kEmpty) {
                 // this lane owns the slot: buffer, then records B and A
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
-#if E2SAR_PROBE_NOAR     // probe build only (not an allocator): offsets from the event number
-                uint64_t boff = (ev % 1024ull) * (need ? need : 256ull);
-#else
                 uint64_t boff = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
-#endif
                 if (boff + blen > R.arenaBytes) {
                     boff = kNoBuf;
                     atomicOr(&R.ctl->errorFlags, 2u);
@@ -718,7 +613,7 @@ __device__ LookupResult find_or_create(const ReasDev &R, bool want, uint64_t ev,
                 active = false;
             }
         }
-        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(E2SAR_REAS_POLL_SLEEP);
+        if (__ballot(waiting)) __builtin_amdgcn_s_sleep(kPollSleep);
 #if E2SAR_TRACE
         pass++;
 #endif
@@ -866,7 +761,7 @@ struct Classified {
 // kernel issues it after its copy, so the copy's waits never sit behind that atomic).
 template <bool DeferAcc = false>
 __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_t stride, bool live,
-                                    uint64_t now, uint32_t shard, bool hasKeys = false, const GroupKeys K = GroupKeys{})
+                                    uint64_t now, uint32_t shard)
 {
     const int lane = threadIdx.x & 63;
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
@@ -907,22 +802,10 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     const bool head = ok && (lane == 0 || !pok || pev != ev || pd != d);
     const bool tail = ok && (lane == 63 || !nok || nev != ev || nd != d);
 
-    // keys resolved by the group-key pre-pass (reas_keys_kernel): a run head whose key is
-    // one of them takes its slot and buffer from the record instead of the table
-    bool pre = false;
-    LookupResult lr{kNoSlot, 0, kNoBuf};
-    if (hasKeys) {
-#pragma unroll
-        for (int k = 0; k < 2; k++)
-            if (!pre && K.valid[k] && ok && ev == K.ev[k] && d == K.d[k]) {
-                pre = true;
-                lr = LookupResult{K.slot[k], K.bytes[k], K.boff[k]};
-            }
-    }
-    {
-        const LookupResult lk = find_or_create(R, head && !pre, ev, d, blen, now);
-        if (!pre) lr = lk;
-    }
+    // (Round 3 tried a group-key pre-pass -- the first and last key of every fused group
+    // resolved by a kernel of its own -- and removed it: -1 us in reas_kernel, +9 us of
+    // pre-pass)
+    const LookupResult lr = find_or_create(R, head, ev, d, blen, now);
 
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
@@ -953,7 +836,7 @@ __device__ Classified classify_wave(const ReasDev &R, const RawHdr &raw, uint32_
     out.rc = ic - hc;
     out.old = 0;
     out.tailAdd = tail && slot != kNoSlot;
-    if (out.tailAdd && !(DeferAcc && sbytes >= (uint32_t)E2SAR_REAS_DEFER_ACC)) {
+    if (out.tailAdd && !(DeferAcc && sbytes >= kDeferAccBytes)) {
         const uint64_t add = ((uint64_t)out.rc << kAccFragShift) | out.rb;
         out.old = atomicAdd(&R.slots[slot].acc, (unsigned long long)add);   // consumed in classify_finish
     }
@@ -1031,12 +914,9 @@ __device__ __forceinline__ void classify_finish(const ReasDev &R, const Classifi
 // Dwords [lo/4, hi/4) of the register chunk v (lo < hi, both multiples of 4) to dst + lo:
 // a payload's first and last 16-byte chunk.  The store instructions a wave issues are what
 // its lanes need between them (exec-masked), so a wave holding one edge lane pays every
-// form the edge takes: E2SAR_EDGE_STORE 0 = one conditional dword store per dword (four
-// store instructions per edge wave, the round-2 form), 1 = one dwordx2 and/or one dword
-// store (two at most), 2 = one store of the edge's length (dword, dwordx2 or dwordx3).
-#ifndef E2SAR_EDGE_STORE
-#define E2SAR_EDGE_STORE 2
-#endif
+// form the edge takes: one store of the edge's length (dword, dwordx2 or dwordx3).  (Round
+// 3, profiles/round3/s3_edge/: four conditional dword stores per edge -- four store
+// instructions per edge wave -- were slower: config 3 scatter 227.6-232.0 vs 225.7-227.7 us.)
 typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
 typedef u32x2 __attribute__((aligned(4))) u32x2_a4;
 typedef uint32_t u32x3 __attribute__((ext_vector_type(3)));
@@ -1054,24 +934,13 @@ __device__ __forceinline__ void st12(uint8_t *p, uint32_t a, uint32_t b, uint32_
 }
 __device__ __forceinline__ void store_dwords(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
 {
-#if E2SAR_EDGE_STORE == 0
-#pragma unroll
-    for (uint32_t d = 0; d < 4; d++)
-        if (4u * d >= lo && 4u * d + 4u <= hi) st4(dst + 4u * d, v[d]);
-#else
     const u32x4 w = rot_down(v, lo >> 2);
     const uint32_t n = (hi - lo) >> 2;
     uint8_t *p = dst + lo;
-#if E2SAR_EDGE_STORE == 1
-    if (n & 2u) st8(p, w.x, w.y);
-    if (n & 1u) st4(p + ((n & 2u) ? 8u : 0u), (n & 2u) ? w.z : w.x);
-#else
     if (n == 3u) st12(p, w.x, w.y, w.z);
     else if (n == 2u) st8(p, w.x, w.y);
     else if (n == 1u) st4(p, w.x);
     else st16u_nt(p, w);
-#endif
-#endif
 }
 
 __device__ __noinline__ void store_bytes(uint8_t *dst, u32x4 v, uint32_t lo, uint32_t hi)
@@ -1144,7 +1013,7 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
         (void)da_window(c, a, pi.hl, stride, sh);
         const u32x4 o = rot_down(x, sh >> 2);
         if (lo == 0u && hi == 16u) {
-            st16_ev(D, o);
+            st16_nt(D, o);
         } else {
             const uint32_t t = hi & ~3u;                               // lo = a is a multiple of 4
             if (lo < t) store_dwords(D, o, lo, t);
@@ -1179,16 +1048,12 @@ struct ReasGroupLds {
 template <int U, bool HO = false, int NT = kBlock>
 __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t g0, uint32_t gn, uint64_t now,
-                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ key)
+                                           uint32_t g, ReasGroupLds &L)
 {
     const uint32_t tx = threadIdx.x;
     const bool w0 = tx < 64;
     const uint32_t lane = tx & 63u;
 
-    // the group's pre-resolved keys (scalar loads, issued first: they ride beside the
-    // header loads instead of a dependent table round trip after them)
-    GroupKeys K{};
-    if (key) K = *key;
     TRACE_AT(0, 0, trace_now());
     // every wave issues the (cached) header loads so no load result crosses a branch
     const RawHdr raw = load_hdr<HO>(R, pkts, stride, lens, g0 + ((lane < gn) ? lane : 0u));
@@ -1238,24 +1103,17 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
             da_store<HO>(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
         }
     };
-    u32x4 x[U];
-#if E2SAR_REAS_PIPE
-    u32x4 y[U];
-#endif
+    u32x4 x[U], y[U];
     // round 0 is in flight while wave 0 classifies.  (A/B, round 4: the first residency
     // wave's groups classifying before their round-0 loads, so their claims do not queue
-    // behind 25 MB of loads, ran 0.5-2 us slower: DESIGN 4.5.)
+    // behind 25 MB of loads, ran 0.5-2 us slower; round 1's loads in flight too -- the
+    // pipeline's second register set live across the classification -- cut occupancy and
+    // lost: DESIGN 4.5.)
     issue(0u, x);
-#if E2SAR_REAS_PIPE && E2SAR_REAS_EARLY
-    // round 1 too (its registers exist for the software pipeline anyway): with 768-thread
-    // workgroups rounds 0 and 1 are the whole group
-    constexpr uint32_t RS0 = (uint32_t)(NT * U);
-    if (RS0 < nch) issue(RS0, y);
-#endif
 
     unsigned long long old = 0;
     if (w0) {
-        const Classified cl = classify_wave<E2SAR_REAS_DEFER_ACC != 0>(R, raw, stride, lane < gn, now, g, key != nullptr, K);
+        const Classified cl = classify_wave<true>(R, raw, stride, lane < gn, now, g);
         L.info[lane] = cl.info;
         old = cl.old;
         L.ev[lane] = cl.ev;
@@ -1271,15 +1129,12 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     lds_barrier();
     TRACE_AT(0, 2, trace_hwid());
 
-#if E2SAR_REAS_PIPE
     // software pipeline: the loads of round r+1 are issued before the stores of round r.
     // Loads, stores and atomics retire from vmcnt in issue order, so a load issued after
     // a store can only be waited for together with that store's write acknowledgement;
     // issued before it, round r+1's data is waited for while round r's stores drain.
     constexpr uint32_t RS = (uint32_t)(NT * U);
-#if !E2SAR_REAS_EARLY
     if (RS < nch) issue(RS, y);
-#endif
     store(0u, x);
     for (uint32_t r0 = RS; r0 < nch; r0 += 2 * RS) {
         if (r0 + RS < nch) issue(r0 + RS, x);
@@ -1288,22 +1143,13 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
         if (r0 + 2 * RS < nch) issue(r0 + 2 * RS, y);
         store(r0 + RS, x);
     }
-#else
-    store(0u, x);
-    for (uint32_t r0 = (uint32_t)(NT * U); r0 < nch; r0 += (uint32_t)(NT * U)) {
-        issue(r0, x);
-        store(r0, x);
-    }
-#endif
 
     if (w0 && L.tail[lane]) {
         Classified cl;
-#if E2SAR_REAS_DEFER_ACC
         // in-order vmcnt: issued before the copy, this atomic's return (slow when ~100 groups
         // of one event add at once) would gate wave 0's first copy wait
-        if (L.bytes[lane] >= (uint32_t)E2SAR_REAS_DEFER_ACC)
+        if (L.bytes[lane] >= kDeferAccBytes)
             old = atomicAdd(&R.slots[L.slot[lane]].acc, ((unsigned long long)L.rc[lane] << kAccFragShift) | L.rb[lane]);
-#endif
         cl.old = old;
         cl.ev = L.ev[lane];
         cl.boff = L.boff[lane];
@@ -1327,8 +1173,7 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 template <int U, bool HO = false, int NT = kBlock>
 __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                            const uint32_t *__restrict__ lens, uint32_t n, uint64_t now, uint32_t G,
-                                           uint32_t g, ReasGroupLds &L, const GroupKeys *__restrict__ keys = nullptr,
-                                           const uint32_t *__restrict__ starts = nullptr)
+                                           uint32_t g, ReasGroupLds &L, const uint32_t *__restrict__ starts = nullptr)
 {
     uint32_t g0 = g * G;
     uint32_t gn = (n - g0 < G) ? n - g0 : G;
@@ -1340,7 +1185,7 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
         if (g1 <= g0 || g1 - g0 > 64u) return;                       // empty or oversized group
         gn = g1 - g0;
     }
-    reas_range<U, HO, NT>(R, pkts, stride, lens, g0, gn, now, g, L, keys ? keys + g : nullptr);
+    reas_range<U, HO, NT>(R, pkts, stride, lens, g0, gn, now, g, L);
 }
 
 // reas_kernel: workgroup b reassembles datagrams [b*G, b*G + G) of the batch.
@@ -1360,68 +1205,20 @@ __device__ __forceinline__ void reas_group(const ReasDev &R, const uint8_t *__re
 // best (71.0 against 73.4-74.0 us at 256 and 71.7 at 768); 1024 threads (one workgroup
 // per CU) lose (82-84 us).
 template <int U, int NT>
-__global__ __launch_bounds__(NT) E2SAR_REAS_WAVES_ATTR void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
-                                                                   uint32_t stride, const uint32_t *__restrict__ lens,
-                                                                   uint32_t n, uint64_t now, uint32_t G,
-                                                                   const GroupKeys *__restrict__ keys,
-                                                                   const uint32_t *__restrict__ starts)
+__global__ __launch_bounds__(NT) void reas_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                  const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
+                                                  uint32_t G, const uint32_t *__restrict__ starts)
 {
     __shared__ ReasGroupLds L;
-    reas_group<U, false, NT>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, keys, starts);
+    reas_group<U, false, NT>(R, pkts, stride, lens, n, now, G, blockIdx.x, L, starts);
 }
 
 // reas_kernel's workgroup size for a slot stride
-constexpr int kReasNTSmall = E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : 768;   // slots of <= 4 KiB
-constexpr int kReasNTJumbo = E2SAR_REAS_THREADS ? E2SAR_REAS_THREADS : 512;
+constexpr int kReasNTSmall = 768;   // slots of <= 4 KiB
+constexpr int kReasNTJumbo = 512;
 __host__ __device__ constexpr int reas_threads(uint32_t stride)
 {
     return stride <= 4096u ? kReasNTSmall : kReasNTJumbo;
-}
-
-// Group-key pre-pass: one lane per key, two keys per reassembly group (its first and last
-// datagram), 32 groups per wave.  Runs of equal keys across consecutive lanes collapse to
-// one table lookup (the run head), so an event spread over ~15 groups costs one CAS here
-// instead of ~15 CASes on its slot in reas_kernel, where each sits in front of a
-// group's stores.  Creates the slots and event buffers exactly as the
-// run heads of reas_kernel would (find_or_create), so the results are the same.
-__global__ __launch_bounds__(kBlock) void reas_keys_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
-                                                           const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
-                                                           uint32_t G, uint32_t nGroups, GroupKeys *__restrict__ keys)
-{
-    const uint32_t lane = threadIdx.x & 63u;
-    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-    const uint32_t g = wave * 32u + (lane >> 1), k = lane & 1u;
-    if (wave * 32u >= nGroups) return;                                   // wave-uniform
-    const bool live = g < nGroups;
-    uint32_t p = 0;
-    if (live) {
-        const uint32_t g0 = g * G, gn = (n - g0 < G) ? n - g0 : G;
-        p = k ? g0 + gn - 1u : g0;
-    }
-    const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
-    const RawHdr raw = load_hdr(R, pkts, stride, lens, p);
-    ParsedHdr h = parse_hdr(raw, hl, stride, live);
-    if (h.ok && foreign_event(R, h.ev)) h.ok = false;
-    const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(h.ev >> 32), 0u) << 32) | lane_prev((uint32_t)h.ev, 0u);
-    const uint32_t pd = lane_prev(h.d, 0u), pok = lane_prev(h.ok ? 1u : 0u, 0u);
-    const bool head = h.ok && (lane == 0 || !pok || pev != h.ev || pd != h.d);
-    const LookupResult lr = find_or_create(R, head, h.ev, h.d, h.blen, now);
-    const uint64_t H = __ballot(head);
-    const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
-    const uint64_t hm = H & le;
-    const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
-    const uint32_t slot = __shfl(lr.slot, myhead);
-    const uint32_t bytes = __shfl(lr.bytes, myhead);
-    const uint64_t boff = shfl_u64(lr.bufOff, myhead);
-    if (live) {
-        GroupKeys *o = keys + g;
-        o->ev[k] = h.ev;
-        o->boff[k] = boff;
-        o->slot[k] = slot;
-        o->bytes[k] = bytes;
-        o->d[k] = h.d;
-        o->valid[k] = (h.ok && slot != kNoSlot) ? 1u : 0u;
-    }
 }
 
 // ---------------------------------------------------------------------------------
@@ -1437,6 +1234,10 @@ __global__ __launch_bounds__(kBlock) void reas_keys_kernel(ReasDev R, const uint
 // no half-empty tail between the two kernels).
 
 #if E2SAR_HIP_EXPERIMENTAL
+// seg blocks of 16 KiB (8-KiB blocks, as seg_kernel uses for 1 MiB events, made the chained
+// launch 147 -> 158 us: twice the blocks at the reassembly occupancy)
+constexpr int kChainSegU = 4;
+
 __device__ __forceinline__ void wait_group_ready(const ReasDev &R, uint32_t *tiles, uint32_t g, uint32_t expect)
 {
     if (threadIdx.x == 0) {
@@ -1462,7 +1263,7 @@ __device__ __forceinline__ void wait_group_ready(const ReasDev &R, uint32_t *til
 }
 
 template <int U>
-__global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(ChainBatches cb, int lbVersion,
+__global__ __launch_bounds__(kBlock) void segreas_kernel(ChainBatches cb, int lbVersion,
                                                                               uint32_t maxPld, uint32_t stride,
                                                                               ReasDev R, uint64_t now)
 {
@@ -1474,14 +1275,14 @@ __global__ __launch_bounds__(kBlock) E2SAR_REAS_WAVES_ATTR void segreas_kernel(C
     const ChainBatch &B = cb.b[b];
     const uint32_t local = blockIdx.x - B.start;
     if (local < B.nSeg) {
-        seg_block<E2SAR_CHAIN_SEG_U, true>(B.events, B.bpe, lbVersion, maxPld, B.pkts, stride, B.lens, nullptr, local,
+        seg_block<kChainSegU, true>(B.events, B.bpe, lbVersion, maxPld, B.pkts, stride, B.lens, nullptr, local,
                                            B.G, B.tiles);
         return;
     }
     const uint32_t g = local - B.nSeg;
     const uint32_t slots = (B.n - g * B.G < B.G) ? B.n - g * B.G : B.G;
     wait_group_ready(R, B.tiles, g, slots * (stride >> 4));
-    reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L, nullptr);
+    reas_group<U, true>(R, B.pkts, stride, B.lens, B.n, now, B.G, g, L);
 }
 
 #endif  // E2SAR_HIP_EXPERIMENTAL
@@ -1530,66 +1331,11 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
     }
 }
 
-// Scatter stores (A/B build knob): 1 = destination-aligned (shift_store: source-aligned
-// loads, the next chunk from the neighbour lane, funnel shift, aligned 16-byte stores); 2 =
-// the same with every lane loading its chunk pair itself; 0 (default) = source-aligned
-// chunks, staged through LDS into aligned stores (lds_stage_store) where scatter_stage()
-// picks it, else stored at their misaligned destination (scatter_chunk).
-#ifndef E2SAR_SCATTER_SHIFT
-#define E2SAR_SCATTER_SHIFT 0
-#endif
-
-// Bytes [s, s+16) of the 32-byte register pair lo:hi (s in 0..15, lane-varying): a funnel
-// shift, v_alignbyte after a dword select.
-__device__ __forceinline__ u32x4 funnel16(u32x4 lo, u32x4 hi, uint32_t s)
-{
-    const uint32_t q = s >> 2, r = s & 3u;
-    const uint32_t w[8] = {lo.x, lo.y, lo.z, lo.w, hi.x, hi.y, hi.z, hi.w};
-    uint32_t t[5];
-#pragma unroll
-    for (int k = 0; k < 5; k++)
-        t[k] = (q == 0u) ? w[k] : (q == 1u) ? w[k + 1] : (q == 2u) ? w[k + 2] : w[k + 3];
-    u32x4 o;
-    o.x = __builtin_amdgcn_alignbyte(t[1], t[0], r);
-    o.y = __builtin_amdgcn_alignbyte(t[2], t[1], r);
-    o.z = __builtin_amdgcn_alignbyte(t[3], t[2], r);
-    o.w = __builtin_amdgcn_alignbyte(t[4], t[3], r);
-    return o;
-}
-
-// Destination-aligned store of the chunk pair (own = datagram bytes [16c, 16c+16), next =
-// [16c+16, 16c+32)) of a classified datagram.  Payload byte t sits at slot offset hl + t
-// and goes to dst + t; with a = dst mod 16, the aligned event block b ((dst & ~15) + 16b)
-// takes slot bytes [hl - a + 16b, +16) = chunk pair (b + q, b + q + 1) shifted by
-// sigma, q = (hl - a) / 16, sigma = (hl - a) mod 16.  So the lane holding chunk c writes
-// block c - q: loads stay source-aligned and independent of the work record (issued
-// before it arrives), stores are aligned 16-byte stores except at the payload's two
-// edges.  Every block of the payload is written by exactly one chunk: the last needs
-// c = nb - 1 + q <= spc - 1 because a + plen <= 16 * spc - 16q.
-__device__ __forceinline__ void shift_store(const PktInfo pi, uint32_t c, u32x4 own, u32x4 next)
-{
-    if (pi.plen == 0u) return;
-    const uint32_t a = (uint32_t)pi.dst & 15u;
-    const uint32_t dlt = pi.hl - a;                              // hl (20 / 36) > 15 >= a
-    const uint32_t q = dlt >> 4;
-    if (c < q) return;
-    const uint32_t b = c - q;
-    if (16u * b >= a + pi.plen) return;                           // past the payload
-    const u32x4 o = funnel16(own, next, dlt & 15u);
-    uint8_t *D = reinterpret_cast<uint8_t *>((pi.dst & ~15ull) + 16ull * b);
-    const uint32_t lo = (b == 0u) ? a : 0u;
-    const uint32_t hi = (a + pi.plen - 16u * b < 16u) ? a + pi.plen - 16u * b : 16u;
-    if (lo == 0u && hi == 16u) {
-        st16_nt(D, o);
-        return;
-    }
-#pragma unroll
-    for (uint32_t d = 0; d < 4; d++)
-        if (4u * d >= lo && 4u * d + 4u <= hi) st4(D + 4u * d, o[d]);
-    const uint32_t l4 = (lo + 3u) & ~3u, h4 = hi & ~3u;          // partial dwords at the edges
-    if (lo < l4) store_bytes(D, o, lo, l4 < hi ? l4 : hi);
-    if (h4 < hi && h4 >= l4) store_bytes(D, o, h4, hi);
-}
+// Scatter stores: source-aligned chunks, staged through LDS into aligned stores
+// (lds_stage_store) where scatter_stage() picks it, else stored at their misaligned
+// destination (scatter_chunk).  (Round 3 measured destination-aligned stores built from
+// neighbour-lane funnel shifts, or from every lane loading its chunk pair: cold leg 2221 /
+// 2020 vs 2369 GiB/s -- what the aligned stores save the extra loads cost)
 
 // Staged scatter (STAGE, chosen per launch by scatter_stage()): the one-round group's
 // source-aligned chunks go through LDS.  Every dword of a payload is written to its destination phase in the group's LDS
@@ -1667,12 +1413,8 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     uint32_t nch = gn * spc;
     const float rspc = 1.0f / (float)spc;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
-    const bool last = (threadIdx.x & 63u) == 63u;
-    u32x4 x[U], xn[U];
+    u32x4 x[U];
     uint32_t pp[U], cc[U];
-    // chunk i of the group: the chunk index space is the slots' bytes, so chunk i + 1 is the
-    // next 16 bytes; a wave's lane 63 loads it itself (its neighbour is in another wave),
-    // every other lane takes it from lane + 1
     auto issue = [&](uint32_t r0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
@@ -1685,9 +1427,6 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
             cc[u] = ic - p * spc;
             const uint8_t *src = bpk + (uint64_t)p * stride + 16u * cc[u];
             x[u] = NT ? ld16_nt(src) : ld16(src);
-            xn[u] = u32x4{0u, 0u, 0u, 0u};
-            if ((E2SAR_SCATTER_SHIFT == 2 || (E2SAR_SCATTER_SHIFT == 1 && last)) && cc[u] + 1u < spc)
-                xn[u] = NT ? ld16_nt(src + 16) : ld16(src + 16);
         }
     };
     issue(0);
@@ -1715,24 +1454,9 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
         if (r0) issue(r0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            // next chunk from lane + 1 (whole wave active: DPP reads every lane)
             const uint32_t i = r0 + (uint32_t)u * kScatBlock + threadIdx.x;
-#if E2SAR_SCATTER_SHIFT == 2
-            if (i >= nch) continue;
-            shift_store(sinfo[pp[u]], cc[u], x[u], xn[u]);          // every lane loaded its pair
-#elif E2SAR_SCATTER_SHIFT == 1
-            u32x4 nx;
-            nx.x = lane_next(x[u].x, 0u);
-            nx.y = lane_next(x[u].y, 0u);
-            nx.z = lane_next(x[u].z, 0u);
-            nx.w = lane_next(x[u].w, 0u);
-            if (last) nx = xn[u];
-            if (i >= nch) continue;
-            shift_store(sinfo[pp[u]], cc[u], x[u], nx);
-#else
             if (i >= nch) continue;
             scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
-#endif
         }
     }
 
@@ -1744,77 +1468,9 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     }
 }
 
-// Chunk-range form of the scatter (G == 0 at launch, E2SAR_SCATTER_RANGE): workgroup blk
-// takes the batch's slot chunks [blk * K, blk * K + K), K = 256 * U, whatever datagrams
-// they belong to -- the loads are a plain linear copy of the slot buffer (pkts + 16 i), the
-// stores go to each chunk's datagram's destination.  At most kRangeSlots datagrams touch one
-// range (the host picks this form only for strides that guarantee it); a datagram's
-// completion is published by the range holding its first chunk.  Against groups of whole
-// datagrams, ranges keep every workgroup's load range 16-KiB and line-aligned: at MTU 9000 a
-// one-datagram group is 561 chunks, a workgroup boundary every 8976 bytes splits a line, and
-// in a microbenchmark the same copy ran 12 % slower (tools/ubench_dgram.hip: slotcopy_g1_u4
-// 202.7 vs lin16 176.6-184.3 us per 590 MB batch).  Measured in the scatter it did not pay
-// (config 3's 590 MB batch 224.7-234.9 vs 228.6-232.0 us; cold leg 2354 vs 2430 GiB/s,
-// profiles/round3/s3_range/), so it is an A/B build (E2SAR_SCATTER_RANGE=1), bit-exact on
-// the GPU suite.
-constexpr uint32_t kRangeSlots = 64;
-template <int U, bool NT>
-__device__ __forceinline__ void scatter_range(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
-                                              uint32_t n, const PktInfo *__restrict__ info,
-                                              const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
-{
-    constexpr uint32_t K = (uint32_t)kScatBlock * U;
-    const uint32_t spc = stride >> 4;
-    const uint64_t total = (uint64_t)n * spc;
-    const uint64_t c0 = (uint64_t)blk * K;
-    const uint32_t nch = (total - c0 < K) ? (uint32_t)(total - c0) : K;
-    const uint32_t p0 = (uint32_t)(c0 / spc);
-    const uint32_t ns = (uint32_t)((c0 + nch - 1u) / spc) - p0 + 1u;   // <= kRangeSlots (host-checked)
-    const uint32_t skew = (uint32_t)(c0 - (uint64_t)p0 * spc);          // chunk of datagram p0 where we start
-    const uint32_t lane = threadIdx.x & 63u;
-    const PktInfo mine = ld_info(info + p0 + ((lane < ns) ? lane : 0u));
-
-    const float rspc = 1.0f / (float)spc;
-    const uint8_t *const base = pkts + 16ull * c0;
-    u32x4 x[U];
-    uint32_t pp[U], cc[U];
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kScatBlock + threadIdx.x;
-        const uint32_t rc = (r < nch) ? r : 0u;
-        const uint32_t l = skew + rc;                                     // chunk index from datagram p0's start
-        uint32_t p = (uint32_t)((float)l * rspc);
-        if (p * spc > l) p--;
-        else if ((p + 1u) * spc <= l) p++;
-        pp[u] = p;
-        cc[u] = l - p * spc;
-        x[u] = NT ? ld16_nt(base + 16u * rc) : ld16(base + 16u * rc);
-    }
-    bool fins = false;
-    if (threadIdx.x < 64) {
-        const uint64_t lo = (uint64_t)R.arena, hi = lo + R.arenaBytes;
-        const bool inside = mine.plen == 0 || (mine.dst >= lo && mine.dst + mine.plen <= hi);
-        const bool own = lane < ns && (lane > 0u || skew == 0u);           // its first chunk is in this range
-        if (own && !inside) atomicOr(&R.ctl->errorFlags, 8u);
-        PktInfo v = (lane < ns && inside) ? mine : PktInfo{0ull, 0u, 0u};
-        fins = own && (v.hl & kPktCompletes) != 0u;
-        v.hl &= ~kPktCompletes;
-        sinfo[lane] = v;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < U; u++) {
-        const uint32_t r = (uint32_t)u * kScatBlock + threadIdx.x;
-        if (r >= nch) continue;
-        scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
-    }
-    if (fins) {
-        const FinishRec f = fin[p0 + lane];
-        const uint32_t fs = f.slot & ~kFinKeepSlot;
-        if (fs < R.tableSlots) complete_event(R, fs, f.ev, f.boff, f.bytes, f.d, f.frags, (f.slot & kFinKeepSlot) != 0u);
-        else atomicOr(&R.ctl->errorFlags, 8u);
-    }
-}
+// (Round 3-4: chunk-range scatter workgroups -- loads exactly a linear 16-KiB range of the
+// slots whatever datagrams they belong to, registers or LDS-staged -- measured no better on
+// config 3 and lost on the cold leg; removed)
 
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,
@@ -1831,8 +1487,7 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_kernel(ReasDev R, con
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    if (G == 0u) scatter_range<U, NT>(R, pkts, stride, n, info, fin, blockIdx.x, sinfo);
-    else scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+    scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
 }
 
 // Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
@@ -1854,8 +1509,7 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
         return;
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
-    if (G == 0u) scatter_range<U, NT>(R, spk, stride, sn, sinfoG, sfin, sb, sinfo);
-    else scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
+    scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2268,29 +1922,37 @@ hipError_t launch_zero_words(void *p, uint64_t nWords, hipStream_t stream)
     return hipGetLastError();
 }
 
-// Launch geometry is fixed at build time: the A/B knobs of earlier rounds are -D flags
-// (tools/build_variants.sh), never environment variables read by the shipped library.
-#ifndef E2SAR_SEG_U
-#define E2SAR_SEG_U 0               // seg_kernel 16-byte chunks per thread: 0 = auto (2 up to 4 MiB of datagrams, else 4)
-#endif
-#ifndef E2SAR_SCATTER_G
-#define E2SAR_SCATTER_G 0           // datagrams per scatter workgroup: 0 = auto (E2SAR_SCATTER_CHUNKS_PER_BLOCK)
-#endif
-#ifndef E2SAR_REAS_BALANCE
-#define E2SAR_REAS_BALANCE 1        // balance reas_kernel groups to whole residency waves
-#endif
-#ifndef E2SAR_SCATTER_LDS
-#define E2SAR_SCATTER_LDS 0         // dynamic LDS per scatter workgroup (occupancy cap); 0 = none
-#endif
-#ifndef E2SAR_PIPE_LDS
-#define E2SAR_PIPE_LDS 0            // same for the pipelined scatter+classify grid
-#endif
-static_assert(E2SAR_SEG_U == 0 || E2SAR_SEG_U == 2 || E2SAR_SEG_U == 4, "seg_kernel is built for U = 2 or 4");
-static_assert(E2SAR_SCATTER_G <= 64 && E2SAR_SCATTER_LDS <= 65536 && E2SAR_PIPE_LDS <= 65536, "knob out of range");
-
-#ifndef E2SAR_SEG_STRIPE
-#define E2SAR_SEG_STRIPE 1          // seg_kernel writes XCD stripes (seg_groups); 0 = linear units (A/B knob)
-#endif
+// Occupancy caps by dynamic LDS: the dynamic LDS that holds a launch of `kernel` (its own
+// static LDS included) to at most perCU workgroups per CU on the current device, from the
+// device's LDS per CU and per workgroup -- 0 (no cap) where the cap cannot be expressed.
+// The caps were measured on gfx950 (160 KiB of LDS per CU); computed here, they mean the
+// same workgroups per CU on any LDS size instead of a fixed byte count.
+template <typename K>
+static size_t occupancy_lds(K kernel, uint32_t perCU)
+{
+    static std::atomic<int> ldsCU[64], ldsWG[64];
+    int dev = 0;
+    if (perCU == 0 || hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+    int cu = ldsCU[dev].load(std::memory_order_relaxed), wg = ldsWG[dev].load(std::memory_order_relaxed);
+    if (cu <= 0 || wg <= 0) {
+        if (hipDeviceGetAttribute(&cu, hipDeviceAttributeMaxSharedMemoryPerMultiprocessor, dev) != hipSuccess ||
+            hipDeviceGetAttribute(&wg, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess || cu <= 0 || wg <= 0) {
+            (void)hipGetLastError();
+            return 0;
+        }
+        ldsCU[dev].store(cu, std::memory_order_relaxed);
+        ldsWG[dev].store(wg, std::memory_order_relaxed);
+    }
+    hipFuncAttributes fa{};
+    if (hipFuncGetAttributes(&fa, reinterpret_cast<const void *>(kernel)) != hipSuccess) {
+        (void)hipGetLastError();
+        return 0;
+    }
+    size_t T = ((size_t)cu / perCU) & ~(size_t)1023;                  // bytes per workgroup
+    if (T > (size_t)wg) T = (size_t)wg;
+    if (T <= fa.sharedSizeBytes || (size_t)cu / T != perCU) return 0;  // perCU fit, perCU + 1 do not
+    return T - fa.sharedSizeBytes;
+}
 
 template <int U, int NT>
 static uint32_t reas_resident_groups();
@@ -2307,8 +1969,8 @@ static bool seg_geom(uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t str
     const uint32_t spc = stride >> 4;
     const uint64_t chunks = (uint64_t)maxPacketsPerEvent * spc;
     if (chunks > 0xFFFFFFFFull || spc == 0) return false;        // chunk index of an event is u32
-    g.U = E2SAR_SEG_U ? (uint32_t)E2SAR_SEG_U : (chunks <= (1u << 18) ? 2u : 4u);
-    g.unitChunks = (uint32_t)E2SAR_SEG_BLOCK * g.U;
+    g.U = chunks <= (1u << 18) ? 2u : 4u;
+    g.unitChunks = (uint32_t)kSegBlock * g.U;
     g.bpe = cdiv(chunks, g.unitChunks);
     g.nUnits = (uint64_t)g.bpe * nEvents;
     // a stripe of about one fused reassembly group, min(49, 9216 / spc) datagrams, then
@@ -2317,11 +1979,10 @@ static bool seg_geom(uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t str
     // the stripe within [3/4, 4/3] of the target (205 x 1 MiB at MTU 1500: 8 -> 9 units,
     // 3383 -> 3007 groups for 2 x 1536 resident)
     g.stripe = 0;
-    if (!E2SAR_SEG_STRIPE) return true;
-    const uint32_t target = std::min<uint32_t>(49u, std::max<uint32_t>(1u, E2SAR_REAS_CHUNKS_PER_BLOCK / spc));
+    const uint32_t target = std::min<uint32_t>(49u, std::max<uint32_t>(1u, kReasChunksPerBlock / spc));
     const uint32_t S0 = std::max<uint32_t>(1u, (uint32_t)((uint64_t)target * spc / g.unitChunks));
     uint32_t best = S0;
-    const uint32_t cap = reas_resident_groups<E2SAR_REAS_U, kBlock>();
+    const uint32_t cap = reas_resident_groups<kReasU, kBlock>();
     if (cap && g.nUnits) {
         const uint64_t waves = ((g.nUnits + S0 - 1) / S0 + cap - 1) / cap;
         uint32_t bestDev = ~0u;
@@ -2348,11 +2009,12 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                                     : sg.nUnits;
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
     if (sg.U == 2)
-        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), E2SAR_SEG_LDS, stream, d_events,
+        hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(kSegBlock), 0, stream, d_events,
                            sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
     else
-        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(E2SAR_SEG_BLOCK), E2SAR_SEG_LDS4, stream, d_events,
-                           sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
+        hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(kSegBlock), occupancy_lds(seg_kernel<4>, kSeg4PerCU),
+                           stream, d_events, sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe,
+                           (uint32_t)sg.nUnits);
     return hipGetLastError();
 }
 
@@ -2462,48 +2124,30 @@ hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvent
     return hipGetLastError();
 }
 
-// Dynamic LDS requested only to cap workgroups per CU (build knobs E2SAR_SCATTER_LDS /
-// E2SAR_PIPE_LDS, default 0 = no cap): fewer bytes in flight shorten the queueing latency
-// that dependent table round trips see.
+// Where the pipelined launch's classify workgroups sit, percent of the way through its
+// scatter workgroups (launch_reas_scatter_classify)
+constexpr uint32_t kPipeClsAtPercent = 75;
 
-
-#ifndef E2SAR_PIPE_CLS_AT
-#define E2SAR_PIPE_CLS_AT 75
-#endif
-static_assert(E2SAR_PIPE_CLS_AT >= 0 && E2SAR_PIPE_CLS_AT <= 100, "percent");
-#ifndef E2SAR_SCATTER_RANGE
-#define E2SAR_SCATTER_RANGE 0       // A/B: scatter workgroups over chunk ranges (1) instead of whole-datagram groups
-#endif
-// Scatter workgroups of the launch: chunk ranges of 256 * U chunks (scatter_range) when at
-// most kRangeSlots datagrams can touch one range, else groups of G whole datagrams.
-// Returns G (0 = ranges) and the workgroup count.
-static uint32_t scatter_group_size(uint32_t stride);
-static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
-{
-    constexpr uint32_t K = (uint32_t)kScatBlock * E2SAR_SCATTER_U;
-    const uint32_t spc = stride >> 4;
-    if (E2SAR_SCATTER_RANGE && !E2SAR_SCATTER_G && spc && (K + spc - 2u) / spc + 1u <= kRangeSlots) {
-        blocks = (uint32_t)(((uint64_t)n * spc + K - 1u) / K);
-        return 0u;
-    }
-    const uint32_t G = scatter_group_size(stride);
-    blocks = cdiv(n, G);
-    return G;
-}
-
+// Scatter workgroups of the launch: groups of G whole datagrams; returns G and the
+// workgroup count.
 static uint32_t scatter_group_size(uint32_t stride)
 {
-    // datagrams per scatter workgroup: at most E2SAR_SCATTER_CHUNKS_PER_BLOCK 16-byte chunks
-    // (one round of 256 threads x 4), <= 64.  The scatter needs no table round trip, so it
+    // datagrams per scatter workgroup: at most kScatterChunksPerBlock 16-byte chunks (one
+    // round of 256 threads x 4), <= 64.  The scatter needs no table round trip, so it
     // streams best in one-round workgroups, like seg_kernel: at 205 x 1 MiB, MTU 1500, a
     // batch read back cold takes 81.5 us with 1K-chunk groups against 100.3 us with the
     // fused kernel's 9K budget (89.5 us at 2K); hot, 68.7 us.
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > E2SAR_SCATTER_CHUNKS_PER_BLOCK * (kScatBlock / kBlock)) G >>= 1;
-    return E2SAR_SCATTER_G ? (uint32_t)E2SAR_SCATTER_G : G;   // build knob: exact datagrams per workgroup
+    while (G > 1 && G * spc > kScatterChunksPerBlock * (kScatBlock / kBlock)) G >>= 1;
+    return G;
 }
-
+static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
+{
+    const uint32_t G = scatter_group_size(stride);
+    blocks = cdiv(n, G);
+    return G;
+}
 
 // Workgroups of reas_kernel<U, NT> the current device holds at once (0 if unknown), per device.
 template <int U, int NT>
@@ -2515,12 +2159,9 @@ static uint32_t reas_resident_groups()
     uint32_t c = cache[dev].load(std::memory_order_relaxed);
     if (c) return c;
     int per = 0, cus = 0;
-    // E2SAR_REAS_BALANCE_LDS: balance on the occupancy the capped launch really gets (A/B knob;
-    // 0 = on the uncapped occupancy, as the caps were measured)
-    const size_t dyn = !E2SAR_REAS_BALANCE_LDS ? 0
-                     : NT == kReasNTSmall      ? (size_t)E2SAR_REAS_SMALL_LDS
-                     : NT == kReasNTJumbo      ? (size_t)E2SAR_REAS_JUMBO_LDS : 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U, NT>, NT, dyn) != hipSuccess ||
+    // the uncapped occupancy, as the jumbo launch's cap was measured (balancing on the
+    // capped one tied, profiles/round4/ab/reas_small_caps.log)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, reas_kernel<U, NT>, NT, 0) != hipSuccess ||
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || per <= 0 || cus <= 0)
         return 0;
     c = (uint32_t)per * (uint32_t)cus;
@@ -2532,12 +2173,12 @@ static uint32_t reas_resident_groups()
 static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG, int NT)
 {
     if (fixedG) return fixedG < 64u ? fixedG : 64u;
-    constexpr int U = E2SAR_REAS_U;
-    // datagrams per workgroup: at most E2SAR_REAS_CHUNKS 16-byte chunks (A/B knob), <= 64.
+    constexpr int U = kReasU;
+    // datagrams per workgroup: at most kReasChunksPerBlock 16-byte chunks, <= 64.
     // (A/B: at MTU 1500 2K-chunk groups lose ~8 %, 1K ~30 %, 4K-12K equal; at MTU 9000 with
     // 8 MiB events 4K chunks (4 datagrams per group) lose 27 % to 9K-18K: per-event counter
     // and table traffic grows with groups per event)
-    const uint32_t spc = stride >> 4, budget = E2SAR_REAS_CHUNKS_PER_BLOCK;
+    const uint32_t spc = stride >> 4, budget = kReasChunksPerBlock;
     uint32_t G = 64;
     while (G > 1 && G * spc > budget) G >>= 1;
     // Balance the launch over whole residency waves: with ceil(n/G) workgroups = 1.5 x
@@ -2548,7 +2189,7 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG, in
     // workgroups on each event's table slot and counter (8 MiB events at MTU 9000 lose
     // 9 % at G 16 -> 10). 205 x 1 MiB at MTU 1500: G 64 -> 49, 2342 -> 3059 groups,
     // reas_kernel 79.0 -> 77.6 us.
-    if (E2SAR_REAS_BALANCE) {
+    {
         const uint32_t cap = NT == kReasNTSmall ? reas_resident_groups<U, kReasNTSmall>()
                            : NT == kReasNTJumbo ? reas_resident_groups<U, kReasNTJumbo>()
                                                 : reas_resident_groups<U, kBlock>();
@@ -2567,30 +2208,27 @@ static uint32_t reas_group_size(uint32_t n, uint32_t stride, uint32_t fixedG, in
     return G;
 }
 
-uint32_t reas_launch_groups(const ReasDev &R, uint32_t n, uint32_t stride)
-{
-    return n ? cdiv(n, reas_group_size(n, stride, R.groupSize, reas_threads(stride))) : 0u;
-}
+// The jumbo-slot launch (512 threads) at most 2 workgroups per CU (16 waves instead of 24):
+// MTU 9000 reas_kernel 71.2 -> 69.3 us (profiles/round4/ab/jumbo_cold_caps.log); the
+// 768-thread launch is at 2 per CU by its registers already, and a cap there changes
+// nothing (reas_caps.log).
+constexpr uint32_t kReasJumboPerCU = 2;
 
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream, GroupKeys *keys)
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream)
 {
-    constexpr int U = E2SAR_REAS_U;
+    constexpr int U = kReasU;
     if (n == 0) return hipSuccess;
     const int NT = reas_threads(stride);
     const uint32_t G = reas_group_size(n, stride, R.groupSize, NT);
     const uint32_t groups = cdiv(n, G);
-    if (keys) {
-        const uint32_t waves = cdiv(groups, 32u);
-        hipLaunchKernelGGL(reas_keys_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, pkts, stride,
-                           lens, n, now, G, groups, keys);
-    }
     if (stride <= 4096u)
-        hipLaunchKernelGGL((reas_kernel<U, kReasNTSmall>), dim3(groups), dim3(kReasNTSmall), E2SAR_REAS_SMALL_LDS, stream, R,
-                           pkts, stride, lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
+        hipLaunchKernelGGL((reas_kernel<U, kReasNTSmall>), dim3(groups), dim3(kReasNTSmall), 0, stream, R,
+                           pkts, stride, lens, n, now, G, (const uint32_t *)nullptr);
     else
-        hipLaunchKernelGGL((reas_kernel<U, kReasNTJumbo>), dim3(groups), dim3(kReasNTJumbo), E2SAR_REAS_JUMBO_LDS, stream, R,
-                           pkts, stride, lens, n, now, G, (const GroupKeys *)keys, (const uint32_t *)nullptr);
+        hipLaunchKernelGGL((reas_kernel<U, kReasNTJumbo>), dim3(groups), dim3(kReasNTJumbo),
+                           occupancy_lds(reas_kernel<U, kReasNTJumbo>, kReasJumboPerCU), stream, R,
+                           pkts, stride, lens, n, now, G, (const uint32_t *)nullptr);
     return hipGetLastError();
 }
 
@@ -2599,24 +2237,24 @@ hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint3
                                     uint32_t n, const uint32_t *starts, uint32_t nGroups, uint64_t now,
                                     hipStream_t stream)
 {
-    constexpr int U = E2SAR_REAS_U;
+    constexpr int U = kReasU;
     if (n == 0 || nGroups == 0) return hipSuccess;
     hipLaunchKernelGGL((reas_kernel<U, kBlock>), dim3(nGroups), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now, 64u,
-                       (const GroupKeys *)nullptr, starts);
+                       starts);
     return hipGetLastError();
 }
 
 hipError_t launch_segreas(ChainBatches cb, int lbVersion, uint32_t maxPld, uint32_t stride, const ReasDev &R,
                           uint64_t now, hipStream_t stream)
 {
-    constexpr int U = E2SAR_REAS_U;
+    constexpr int U = kReasU;
     if (cb.nb == 0 || cb.nb > kChainMaxBatches) return hipErrorInvalidValue;
     uint64_t grid = 0;
     for (uint32_t b = 0; b < cb.nb; b++) {
         ChainBatch &B = cb.b[b];
         const uint64_t chunks = (uint64_t)B.maxPacketsPerEvent * (stride >> 4);
         if (chunks > 0xFFFFFFFFull) return hipErrorInvalidValue;
-        B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * E2SAR_CHAIN_SEG_U) : 0u;
+        B.bpe = (B.nEvents && B.n) ? cdiv(chunks, (uint64_t)kBlock * kChainSegU) : 0u;
         B.G = B.n ? reas_group_size(B.n, stride, R.groupSize, kBlock) : 1u;
         B.start = (uint32_t)grid;
         B.nSeg = B.bpe * B.nEvents;
@@ -2649,31 +2287,24 @@ hipError_t launch_reas_classify(const ReasDev &R, const uint8_t *pkts, uint32_t 
 // 123.0-123.6 vs 125.2-125.4 us; but the cold leg at MTU 1500 (8-datagram groups read from
 // HBM, where the LDS barrier waits for the slowest of the group's loads) 84.9-85.5 vs
 // 83.0-83.3 us.  So: staged unless the datagrams stream in at small strides.
-#ifndef E2SAR_SCATTER_STAGE
-#define E2SAR_SCATTER_STAGE 1       // A/B: 0 = never stage
-#endif
-static bool scatter_stage(uint32_t stride, bool nt)
-{
-    return E2SAR_SCATTER_STAGE && E2SAR_SCATTER_SHIFT == 0 && (!nt || stride > 2048u);
-}
+static bool scatter_stage(uint32_t stride, bool nt) { return !nt || stride > 2048u; }
 
-// Dynamic LDS of an unstaged streaming scatter launch (cold datagrams at small strides): an
-// occupancy cap of 6 workgroups per CU instead of 8.  Round 4, cold leg at MTU 1500
+// An unstaged streaming scatter launch (cold datagrams at small strides) at most 6
+// workgroups per CU instead of 8.  Round 4, cold leg at MTU 1500
 // (profiles/round4/ab/scatter_occupancy.log): 82.7 vs 83.5-83.9 us per pipelined launch at
 // 6 per CU, 84.8-86.0 at 5, 88.0-88.8 at 4; staged launches (their own 18 KiB of LDS) lose
 // with any cap (config 3 284-286 vs 232 us at 3 per CU), so they keep none.
-#ifndef E2SAR_COLD_SCATTER_LDS
-#define E2SAR_COLD_SCATTER_LDS 24576
-#endif
-static size_t scatter_lds(bool stage, bool nt, size_t knob)
+constexpr uint32_t kColdScatterPerCU = 6;
+template <typename K>
+static size_t scatter_lds(K kernel, bool stage, bool nt)
 {
-    return (!stage && nt && knob == 0) ? (size_t)E2SAR_COLD_SCATTER_LDS : knob;
+    return (!stage && nt) ? occupancy_lds(kernel, kColdScatterPerCU) : 0;
 }
 
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
                                const void *work, hipStream_t stream, bool nt)
 {
-    constexpr int U = E2SAR_SCATTER_U;
+    constexpr int U = kScatU;
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     uint32_t blocks = 0;
@@ -2681,9 +2312,9 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const PktInfo *info = reinterpret_cast<const PktInfo *>(w);
     const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
     const bool st = scatter_stage(stride, nt);
-    const size_t lds = scatter_lds(st, nt, E2SAR_SCATTER_LDS);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), lds, stream, R, pkts, stride, n, G, info, fin);
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, pkts, stride,
+                           n, G, info, fin);
     };
     if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
     else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
@@ -2694,7 +2325,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
                                         uint64_t now, void *cwork, hipStream_t stream, bool nt)
 {
-    constexpr int U = E2SAR_SCATTER_U;
+    constexpr int U = kScatU;
     if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream, nt);
     if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
     const uint8_t *sw = static_cast<const uint8_t *>(swork);
@@ -2702,17 +2333,17 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint32_t sblocks = 0;
     const uint32_t G = scatter_geometry(stride, sn, sblocks);
     const uint32_t nCls = cdiv(cn, kScatBlock);
-    // where the classify workgroups sit in the grid: E2SAR_PIPE_CLS_AT percent of the way
+    // where the classify workgroups sit in the grid: kPipeClsAtPercent of the way
     // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
     // workgroup slots through their dependent round trips while the scatter ramps up; three
     // quarters of the way in they run beside the scatter's last quarter and finish with it
     // (cold leg, 205 x 1 MiB: 81.4-83.8 vs 83.9-87.0 us per launch over three boxes, 50 / 65 /
     // 80 / 88 % in between; profiles/round3/s3_cls/)
-    const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * E2SAR_PIPE_CLS_AT / 100u);
+    const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * kPipeClsAtPercent / 100u);
     const bool st = scatter_stage(stride, nt);
-    const size_t lds = scatter_lds(st, nt, E2SAR_PIPE_LDS);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), lds, stream, R, stride, spk, sn, G,
+        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, stride,
+                           spk, sn, G,
                            reinterpret_cast<const PktInfo *>(sw),
                            reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
                            reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,
@@ -2890,13 +2521,7 @@ __global__ __launch_bounds__(kBlock) void route_scan_kernel(uint32_t *__restrict
 // A/B at 205 x 1 MiB, MTU 1500, spread landing (route = hist + scan + pack, per batch):
 // split 1/2/4/8 -> 97/92/100/116 us with non-temporal datagram loads, which also leave the
 // Infinity Cache to the packed copy that reassembly reads next (reas 108 -> 79 us).
-#ifndef E2SAR_PACK_SPLIT
-#define E2SAR_PACK_SPLIT 2
-#endif
-constexpr uint32_t kPackSplit = E2SAR_PACK_SPLIT;
-#ifndef E2SAR_PACK_POL
-#define E2SAR_PACK_POL 2      // bit 0: non-temporal stores, bit 1: non-temporal loads
-#endif
+constexpr uint32_t kPackSplit = 2;
 __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__restrict__ pkts, uint32_t stride,
                                                             const uint32_t *__restrict__ lens, uint32_t n, int withLB,
                                                             uint32_t world, uint32_t self, int excludeSelf,
@@ -2952,15 +2577,13 @@ __global__ __launch_bounds__(kBlock) void route_pack_kernel(const uint8_t *__res
             qq[u] = (i < c1) ? pos[k] : kNoDest;                       // kNoDest: stays here
             x[u] = u32x4{0u, 0u, 0u, 0u};
             if (qq[u] != kNoDest)
-                x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
-                                             : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+                x[u] = ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
         }
 #pragma unroll
         for (int u = 0; u < UR; u++) {
             if (qq[u] != kNoDest) {
                 uint8_t *o = out + (uint64_t)qq[u] * stride + 16u * cc[u];
-                if (E2SAR_PACK_POL & 1) st16_nt(o, x[u]);
-                else st16(o, x[u]);
+                st16(o, x[u]);
             }
         }
     }
@@ -3029,15 +2652,13 @@ __global__ __launch_bounds__(kBlock) void route_append_kernel(const uint8_t *__r
             qq[u] = (i < nch) ? pos[k] : kNoDest;
             x[u] = u32x4{0u, 0u, 0u, 0u};
             if (qq[u] != kNoDest)
-                x[u] = (E2SAR_PACK_POL & 2) ? ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u])
-                                             : ld16(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
+                x[u] = ld16_nt(pkts + (uint64_t)(p0 + k) * stride + 16u * cc[u]);
         }
 #pragma unroll
         for (int u = 0; u < UR; u++) {
             if (qq[u] != kNoDest) {
                 uint8_t *o = out + (uint64_t)qq[u] * stride + 16u * cc[u];
-                if (E2SAR_PACK_POL & 1) st16_nt(o, x[u]);
-                else st16(o, x[u]);
+                st16(o, x[u]);
             }
         }
     }

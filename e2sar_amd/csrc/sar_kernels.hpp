@@ -105,22 +105,6 @@ struct ReasDev {
     uint32_t groupSize;       // datagrams per reas_kernel workgroup (config), 0 = chip-balanced auto
 };
 
-// Group-key pre-pass of the fused reassembly (reas_keys_kernel): for reassembly group g the
-// keys of its first and last datagram, resolved in the event table before reas_kernel runs
-// (slot created or found, event buffer allocated).  reas_kernel loads the record beside
-// the group's headers, and lanes whose (eventNum, dataId) equals one of the two keys skip
-// the table lookup; any other lane (a third event inside the group, a bad header) looks up
-// as before.  valid[k] = 0: key k did not parse or the lookup failed.  64 bytes.
-struct GroupKeys {
-    uint64_t ev[2];
-    uint64_t boff[2];
-    uint32_t slot[2];
-    uint32_t bytes[2];
-    uint32_t d[2];
-    uint32_t valid[2];
-};
-static_assert(sizeof(GroupKeys) == 64, "one 64-byte record per group");
-
 // Per-datagram result of classification (held in LDS between the two phases of reas_kernel).
 struct PktInfo {
     uint64_t dst;     // device address of the payload's destination (0 = drop)
@@ -206,17 +190,14 @@ hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
 hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvents, uint32_t maxPld,
                              uint64_t lbTick, uint32_t entropyBase, e2sar_hip_seg_event *d_events,
                              uint32_t *d_counts, hipStream_t stream);
-// keys (optional, reas_launch_groups() records): run the group-key pre-pass first
 hipError_t launch_reassemble(const ReasDev &R, const uint8_t *pkts, uint32_t stride,
-                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream,
-                             GroupKeys *keys = nullptr);
+                             const uint32_t *lens, uint32_t n, uint64_t now, hipStream_t stream);
 // XCD-matched groups of a planned batch (seg_kernel's stripes) and the fused reassembly over them
 uint32_t seg_groups(const e2sar_hip_seg_event *ev, uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t maxPld,
                     uint32_t stride, uint32_t *starts, uint32_t cap);
 hipError_t launch_reassemble_groups(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                                     uint32_t n, const uint32_t *starts, uint32_t nGroups, uint64_t now,
                                     hipStream_t stream);
-uint32_t reas_launch_groups(const ReasDev &R, uint32_t n, uint32_t stride);   // workgroups of reas_kernel
 // Chained form: segment each batch and reassemble the same datagrams, up to
 // kChainMaxBatches batches in one launch (segreas_kernel).  Batch b: nEvents descriptors at
 // events (pktBase from seg_plan), n datagrams into pkts/lens, tiles = n zeroed words (left

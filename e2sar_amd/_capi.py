@@ -243,13 +243,34 @@ def has_experimental() -> bool:
     device.  So a test module's skip marker, evaluated at collection, must not load it."""
     if _lib is not None:
         return all(hasattr(_lib, n) for n in EXPERIMENTAL_SIGNATURES)
-    import subprocess
-    try:
-        out = subprocess.run(["nm", "-D", "--defined-only", LIB_PATH], capture_output=True, text=True,
-                             timeout=30).stdout
-    except (OSError, subprocess.SubprocessError):
+    if not os.path.exists(LIB_PATH):
         return False
-    return all(f" T {n}\n" in out + "\n" for n in EXPERIMENTAL_SIGNATURES)
+    return set(EXPERIMENTAL_SIGNATURES) <= elf_defined_symbols(LIB_PATH)
+
+
+def elf_defined_symbols(path: str) -> set:
+    """Names of the symbols an ELF64 little-endian shared library defines (its .dynsym
+    entries with a section index), read from the file -- no loader, no binutils."""
+    import struct
+    with open(path, "rb") as f:
+        data = f.read()
+    if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+        raise ValueError(f"{path}: not an ELF64 little-endian file")
+    shoff, = struct.unpack_from("<Q", data, 0x28)
+    shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+    sections = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + k * shentsize) for k in range(shnum)]
+    out = set()
+    for name, typ, _fl, _addr, off, size, link, _info, _al, entsize in sections:
+        if typ != 11 or not entsize:                            # SHT_DYNSYM
+            continue
+        stroff = sections[link][4]
+        for k in range(size // entsize):
+            st_name, _st_info, _st_other, st_shndx = struct.unpack_from("<IBBH", data, off + k * entsize)
+            if st_shndx == 0 or st_name == 0:                   # undefined / unnamed
+                continue
+            end = data.index(b"\0", stroff + st_name)
+            out.add(data[stroff + st_name:end].decode())
+    return out
 
 
 def need_experimental(what: str) -> None:

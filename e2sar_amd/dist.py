@@ -269,6 +269,11 @@ class SpreadPipeline:
         """in_place=False routes every landed datagram, this rank's own included, through the
         exchange (no in-place reassembly): the route-all form, which also drives the whole
         RCCL data path at world 1."""
+        if depth < 2:
+            # a region set is reused only after the exchange that reads it was issued, which
+            # happens one land() later: with one set, land() would reset and refill it under
+            # the previous batch's pending all_to_all
+            raise ValueError("SpreadPipeline needs depth >= 2 (region / receive sets in rotation)")
         self.ctx, self.R, self.stride, self.max_batch = ctx, R, stride, max_batch
         self.world, self.rank, self.group, self.depth = world, rank, group, depth
         self.in_place = in_place

@@ -334,6 +334,12 @@ class DeviceReassembler:
             C.c_void_p(c_packets.data_ptr()), C.c_void_p(c_lens.data_ptr()), c_n, int(now_ms),
             C.c_void_p(c_work.data_ptr()), c_work.numel(), C.c_void_p(_stream_handle(stream))))
 
+    def forget_stream(self, stream: torch.cuda.Stream) -> None:
+        """Before the caller destroys `stream`, on which it launched through this reassembler:
+        wait for it, stop tracking it and free its internal buffers
+        (e2sar_hip_reas_forget_stream).  The stream must still be alive."""
+        check(lib().e2sar_hip_reas_forget_stream(self._h, C.c_void_p(_stream_handle(stream))))
+
     def gc(self, now_ms: int, timeout_ms: int, stream: Optional[torch.cuda.Stream] = None) -> None:
         check(lib().e2sar_hip_reas_gc(self._h, int(now_ms), int(timeout_ms), C.c_void_p(_stream_handle(stream))))
 

@@ -401,8 +401,10 @@ int e2sar_hip_reas_set_cold(e2sar_hip_reas *r, int cold);
  * reassembler was ever captured).  Snapshots (poll, lost_poll, get_stats) wait for every
  * stream the reassembler launched on, so a stream must outlive the reassembler's last
  * snapshot unless it is forgotten first: HIP may hand a destroyed stream's handle to a new
- * stream.  (A snapshot that finds a handle already invalid drops it the same way.)  No
- * reference counterpart: the reference's receive threads own their sockets for their life. */
+ * stream.  (A snapshot that finds a handle already invalid drops it the same way.)  The
+ * stream must still be alive when this is called (it is synchronised): call it, then
+ * destroy the stream -- never the other way round.  No reference counterpart: the
+ * reference's receive threads own their sockets for their life. */
 int e2sar_hip_reas_forget_stream(e2sar_hip_reas *r, void *stream);
 
 #ifdef __cplusplus

@@ -101,9 +101,12 @@ size_t e2o_segment_batch(const uint8_t *events, size_t n, size_t bytes,
 
 /* ---- CPU baseline timing (cpu_bench.c; bench.py's cpu_baseline leg only) ----
  * `threads` POSIX threads each segment + reassemble the nEvents-event sample until
- * `seconds` have passed; returns 0 with the payload bytes done and the wall time. */
+ * `seconds` have passed; returns 0 with the payload bytes done and the wall time.
+ * ringBytes: 0 = each thread reuses one datagram buffer and one event block (cache-resident);
+ * > 0 = per-thread rings of at least ringBytes of datagrams and of live events (DRAM). */
 int e2o_cpu_bench(const uint8_t *events, size_t nEvents, size_t bytes, int lbHdrVersion, size_t maxPldLen,
-                  uint16_t dataId, int threads, double seconds, uint64_t *bytesDone, double *elapsed);
+                  uint16_t dataId, int threads, double seconds, size_t ringBytes, uint64_t *bytesDone,
+                  double *elapsed);
 
 #ifdef __cplusplus
 }

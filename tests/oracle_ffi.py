@@ -73,7 +73,7 @@ def lib() -> C.CDLL:
         L.e2o_reas_get_stats.restype = None
         L.e2o_reas_get_stats.argtypes = [vp, C.POINTER(Stats)]
         L.e2o_cpu_bench.restype = C.c_int
-        L.e2o_cpu_bench.argtypes = [u8p, sz, sz, C.c_int, sz, C.c_uint16, C.c_int, C.c_double,
+        L.e2o_cpu_bench.argtypes = [u8p, sz, sz, C.c_int, sz, C.c_uint16, C.c_int, C.c_double, sz,
                                     C.POINTER(C.c_uint64), C.POINTER(C.c_double)]
         _lib = L
     return _lib

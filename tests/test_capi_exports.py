@@ -50,6 +50,30 @@ def test_experimental_forms_are_not_in_the_product():
         assert not set(exp) & exported
 
 
+def test_elf_symbol_reader_matches_nm():
+    """has_experimental() reads the library's .dynsym in Python (no binutils on the path, no
+    load before torch); it must see what nm sees, and tell the product library from the
+    experimental one."""
+    import shutil
+    from e2sar_amd import _capi
+    mine = {n for n in _capi.elf_defined_symbols(_capi.LIB_PATH) if n.startswith("e2sar_hip_")}
+    assert set(declared_functions()) <= mine
+    if shutil.which("nm"):
+        out = subprocess.run(["nm", "-D", "--defined-only", _capi.LIB_PATH], capture_output=True, text=True).stdout
+        assert mine == set(re.findall(r" [TW] (e2sar_hip_\w+)", out))
+    if _capi.LIB_PATH.endswith("lib/libe2sar_hip.so"):
+        assert not _capi.has_experimental()
+    exp_lib = os.path.join(ROOT, "build", "variants", "lib_experimental.so")
+    if os.path.exists(exp_lib):
+        assert set(_capi.EXPERIMENTAL_SIGNATURES) <= _capi.elf_defined_symbols(exp_lib)
+
+
+def test_spread_pipeline_rejects_depth_one():
+    from e2sar_amd.dist import SpreadPipeline
+    with pytest.raises(ValueError, match="depth >= 2"):
+        SpreadPipeline(None, None, 1472, 16, 2, 0, depth=1)
+
+
 def test_host_geometry_matches_oracle():
     from e2sar_amd import _capi
     L = _capi.lib()

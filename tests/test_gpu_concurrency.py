@@ -206,3 +206,44 @@ def test_bench_scale_graph_roundtrip(hip):
                if r.numFragments != npk or r.bytes != B
                or not torch.equal(arena[r.arenaOffset: r.arenaOffset + B], src[r.eventNum, :B])]
         assert not bad, (rep, bad[:8])
+
+
+def test_forget_stream_then_destroy(hip):
+    """e2sar_hip_reas_forget_stream: reassemble on a stream of our own (reference-order mode,
+    so the stream gets internal scratch), forget it, destroy it, then launch on a fresh
+    stream (HIP may reuse the handle) and snapshot -- every event and counter as the oracle's."""
+    import ctypes as C
+    torch = _torch()
+    from e2sar_amd import _capi, sar
+    from e2sar_amd._capi import check, lib
+    B, n_ev = 100_000, 6
+    src = _source(hip, n_ev, B, 0xF0F0)
+    seg, plan, pk, ln = _segment(hip, src, B, 1500)
+    stride, n = seg.stride, plan.total_packets
+    half = n // 2
+    R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=64, arena_bytes=n_ev * B + 4096,
+                              flags=_capi.REAS_REFERENCE_ORDER)
+    torch.cuda.synchronize()
+    s1 = C.c_void_p()
+    check(lib().e2sar_hip_stream_create(0, C.byref(s1)))
+    check(lib().e2sar_hip_reassemble_batch(R.handle, C.c_void_p(pk.data_ptr()), stride, C.c_void_p(ln.data_ptr()),
+                                           half, 0, s1))
+    check(lib().e2sar_hip_reas_forget_stream(R.handle, s1))          # waits for s1, drops its scratch
+    check(lib().e2sar_hip_stream_destroy(s1))
+    s2 = C.c_void_p()
+    check(lib().e2sar_hip_stream_create(0, C.byref(s2)))
+    check(lib().e2sar_hip_reassemble_batch(R.handle, C.c_void_p(pk[half * stride:].data_ptr()), stride,
+                                           C.c_void_p(ln[half:].data_ptr()), n - half, 0, s2))
+    recs = R.poll()                                                 # waits for s2 (and not for s1)
+    st = R.stats()
+    ost, ofr = _oracle_stats(pk, ln, n, stride)
+    assert {(r.eventNum, r.dataId) for r in recs} == set(ofr)
+    for f in ("eventSuccess", "totalPackets", "totalBytes", "badHeaderDiscards", "dataErrCnt"):
+        assert getattr(st, f) == ost[f], f
+    arena = R.arena_tensor()
+    for r in recs:
+        assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], src[r.eventNum, :B])
+    R.forget_stream(torch.cuda.current_stream())                    # the Python wrapper
+    check(lib().e2sar_hip_reas_forget_stream(R.handle, s2))
+    check(lib().e2sar_hip_stream_destroy(s2))
+    assert R.stats().eventSuccess == ost["eventSuccess"]

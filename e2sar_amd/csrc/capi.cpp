@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <deque>
@@ -50,10 +51,18 @@ int hip_fail(hipError_t e, const char *what)
 
 }  // namespace
 
+// A context is shared: every reassembler created on it holds a reference, so the caller may
+// destroy the context and its reassemblers in any order (a garbage collector tearing down a
+// reference cycle picks one) -- the memory goes with the last reference.
 struct e2sar_hip_ctx {
     int device = 0;
     hipStream_t stream = nullptr;
+    std::atomic<int> refs{1};
 };
+static void ctx_release(e2sar_hip_ctx *c)
+{
+    if (c && c->refs.fetch_sub(1, std::memory_order_acq_rel) == 1) delete c;
+}
 
 struct e2sar_hip_reas {
     e2sar_hip_ctx *ctx = nullptr;
@@ -204,7 +213,7 @@ void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx)
     if (!ctx) return;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
-    delete ctx;
+    ctx_release(ctx);
 }
 
 int e2sar_hip_stream_create(int device, void **out)
@@ -557,6 +566,7 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
         reas_release(r);
         return hip_fail(e, "state init");
     }
+    ctx->refs.fetch_add(1, std::memory_order_relaxed);          // released by e2sar_hip_reas_destroy
     *out = r;
     return E2SAR_HIP_OK;
 }
@@ -578,7 +588,9 @@ void e2sar_hip_reas_destroy(e2sar_hip_reas *r)
     (void)hipFree(r->dev.arena);
     (void)hipFree(r->stateMem);
     free_internal(r);
+    e2sar_hip_ctx *ctx = r->ctx;
     delete r;
+    ctx_release(ctx);
 }
 
 uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r) { return r ? r->dev.arena : nullptr; }

@@ -58,6 +58,8 @@ int e2sar_hip_ctx_create(int device, void *stream, e2sar_hip_ctx **out);
 /* A non-blocking stream for callers without a HIP toolchain. */
 int e2sar_hip_stream_create(int device, void **out);
 int e2sar_hip_stream_destroy(void *stream);
+/* Every reassembler created on a context holds a reference to it: a context and its
+ * reassemblers may be destroyed in any order (the memory goes with the last of them). */
 void e2sar_hip_ctx_destroy(e2sar_hip_ctx *ctx);
 void *e2sar_hip_ctx_stream(e2sar_hip_ctx *ctx);
 int e2sar_hip_ctx_device(e2sar_hip_ctx *ctx);

@@ -243,7 +243,31 @@ def test_forget_stream_then_destroy(hip):
     arena = R.arena_tensor()
     for r in recs:
         assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], src[r.eventNum, :B])
-    R.forget_stream(torch.cuda.current_stream())                    # the Python wrapper
+    ts = torch.cuda.Stream()                                        # the Python wrapper
+    R.gc(now_ms=1, timeout_ms=1 << 40, stream=ts)
+    R.forget_stream(ts)
     check(lib().e2sar_hip_reas_forget_stream(R.handle, s2))
     check(lib().e2sar_hip_stream_destroy(s2))
     assert R.stats().eventSuccess == ost["eventSuccess"]
+
+
+def test_context_destroyed_before_its_reassembler(hip):
+    """A garbage collector tearing down a reference cycle destroys a Context and the
+    DeviceReassembler made on it in either order; the reassembler holds a reference on the
+    context (capi.cpp), so reas_destroy never reads a freed context (it once set the device
+    from one: 'invalid device ordinal' on the next HIP call of the process)."""
+    torch = _torch()
+    from e2sar_amd import sar
+    for first in ("ctx", "reas"):
+        ctx = sar.Context(0)
+        R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=64, arena_bytes=1 << 20)
+        R.recycle(force=True)
+        torch.cuda.synchronize()
+        if first == "ctx":
+            ctx.close()
+            R.close()
+        else:
+            R.close()
+            ctx.close()
+        x = torch.full((64,), 7, dtype=torch.int32, device=hip.torch_device)
+        assert torch.equal(x, x.clone())                          # the process is still healthy

@@ -78,8 +78,8 @@ def _spread_rank(rank, world, mode, corrupt=True):
     hp_l = lpk[: nl * stride].view(nl, stride).cpu().numpy()
     hl_l = lln[:nl].cpu().numpy().astype(np.uint32)
     if mode in ("pipeline", "pipeline_all"):
-        # dist.SpreadPipeline (bench.py's spread sub-leg): two landed batches (a cut inside
-        # events), each reassembled in place and routed, its exchange and the reassembly of
+        # dist.SpreadPipeline (bench.py's spread sub-leg): landed batches, each reassembled in
+        # place and routed, its exchange and the reassembly of
         # what it brought on their own streams (RCCL) or synchronous (gloo); pipeline_all
         # routes every datagram, own included, through the exchange
         from e2sar_amd.dist import SpreadPipeline
@@ -88,15 +88,30 @@ def _spread_rank(rank, world, mode, corrupt=True):
             R.set_owner(world, rank)
         pipe = SpreadPipeline(ctx, R, stride, nl, world, rank, in_place=in_place)
         R.set_cold(True)
+        # what each exchange brought, copied on the stream that reassembles it (the receive
+        # sets rotate, so a later batch overwrites them)
+        arrived = []
+        reas_rx = pipe._reassemble_received
+
+        def keep_copy(rpk_, rln_, n_, work_, stream_):
+            with torch.cuda.stream(stream_ if stream_ is not None else torch.cuda.current_stream()):
+                arrived.append((rpk_[: n_ * stride].clone(), rln_[:n_].clone()))
+            reas_rx(rpk_, rln_, n_, work_, stream_)
+
+        pipe._reassemble_received = keep_copy
         pipe.begin_step()
-        cut = nl // 3 + 1
-        for a, b in ((0, cut), (cut, nl)):
-            pipe.land(lpk[a * stride:], lln[a:], b - a)
+        # five batches (cuts inside events): with the default depth 3 the exchanges of the
+        # first three are issued by later land() calls and region / receive sets are reused
+        cuts = [0] + [nl * k // 5 + k for k in range(1, 5)] + [nl]
+        for a, b in zip(cuts[:-1], cuts[1:]):
+            if b > a:
+                pipe.land(lpk[a * stride:], lln[a:], b - a)
         pipe.flush()
         torch.cuda.synchronize()
         nr = sum(c for _, c in pipe.recv_log)
-        rpk = torch.cat([pipe.recv[sl][0][: c * stride] for sl, c in pipe.recv_log] + [lpk[:0]])
-        rln = torch.cat([pipe.recv[sl][1][:c] for sl, c in pipe.recv_log] + [lln[:0]])
+        assert nr == sum(x[1].numel() for x in arrived)
+        rpk = torch.cat([x[0] for x in arrived] + [lpk[:0]])
+        rln = torch.cat([x[1] for x in arrived] + [lln[:0]])
         counts = [sum(m[rank][d] for m in pipe.matrices) for d in range(world)]
         keep = []
         for k in range(nl):

@@ -1472,6 +1472,27 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
 // slots whatever datagrams they belong to, registers or LDS-staged -- measured no better on
 // config 3 and lost on the cold leg; removed)
 
+// XCD-aware visit order of the scatter forms (round 5).  Workgroup b of a launch runs on XCD
+// b mod 8 (round-robin dispatch; a speed assumption only, never correctness).  In dispatch
+// order, consecutive scatter groups -- one 8976-byte datagram at MTU 9000, eight at 1500 --
+// sat on different XCDs, so every group boundary (a 128-byte slot line shared by two
+// datagrams, and at the destination a line shared by two payloads) was touched by two
+// XCDs' L2s.  Here each XCD takes runs of kXcdRun consecutive groups, the eight XCDs' runs
+// side by side, so the launch still moves through the batch as one front.  Config 3 (70 x 8
+// MiB at MTU 9000, 65,730 one-datagram groups): split reassembly 231-234 -> 211-213 us with
+// runs of 128 (32-128 within 2 us; 8 or 16 contiguous regions, one per XCD, 221-224 us;
+// spreading the groups in flight over 64-70 regions 236-246 us), cold leg at MTU 1500
+// unchanged within noise (profiles/round5/xcd_order/).  A bijection on [0, nb): the last
+// nb mod (8 kXcdRun) groups keep their order.
+constexpr uint32_t kXcdRun = 128;
+__device__ __forceinline__ uint32_t xcd_runs(uint32_t b, uint32_t nb)
+{
+    constexpr uint32_t W = 8u * kXcdRun;
+    if (b >= nb / W * W) return b;
+    const uint32_t w = b % W;
+    return (b - w) + (w % 8u) * kXcdRun + w / 8u;
+}
+
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,
                                                                uint32_t n, uint64_t now, PktInfo *__restrict__ info,
@@ -1487,12 +1508,12 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_kernel(ReasDev R, con
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, blockIdx.x, sinfo);
+    scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, xcd_runs(blockIdx.x, (n + G - 1u) / G), sinfo);
 }
 
-// Pipelined form: workgroups [0, nClsBlocks) classify batch b+1, the rest scatter batch b.
-// The classify workgroups have the low indices so they are dispatched first and their
-// round trips start while the scatter workgroups fill the machine.
+// Pipelined form: workgroups [clsStart, clsStart + nClsBlocks) classify batch b+1, the rest
+// scatter batch b (in xcd_runs order: clsStart and nClsBlocks are multiples of 8, so a
+// scatter workgroup's index keeps its XCD parity).
 template <int U, bool NT, bool STAGE>
 __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
@@ -1501,7 +1522,7 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     FinishRec *__restrict__ cfin, uint32_t nClsBlocks, uint32_t clsStart)
 {
     __shared__ PktInfo sinfo[64];
-    // workgroups [clsStart, clsStart + nClsBlocks) classify, the others scatter in order
+    // workgroups [clsStart, clsStart + nClsBlocks) classify, the others scatter
     const uint32_t b = blockIdx.x;
     if (b - clsStart < nClsBlocks) {
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
@@ -1509,7 +1530,7 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
         return;
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
-    scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, sb, sinfo);
+    scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, xcd_runs(sb, (sn + G - 1u) / G), sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2332,14 +2353,14 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     uint32_t sblocks = 0;
     const uint32_t G = scatter_geometry(stride, sn, sblocks);
-    const uint32_t nCls = cdiv(cn, kScatBlock);
+    const uint32_t nCls = (cdiv(cn, kScatBlock) + 7u) & ~7u;     // multiples of 8: see xcd_runs
     // where the classify workgroups sit in the grid: kPipeClsAtPercent of the way
     // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
     // workgroup slots through their dependent round trips while the scatter ramps up; three
     // quarters of the way in they run beside the scatter's last quarter and finish with it
     // (cold leg, 205 x 1 MiB: 81.4-83.8 vs 83.9-87.0 us per launch over three boxes, 50 / 65 /
     // 80 / 88 % in between; profiles/round3/s3_cls/)
-    const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * kPipeClsAtPercent / 100u);
+    const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * kPipeClsAtPercent / 100u) & ~7u;
     const bool st = scatter_stage(stride, nt);
     auto go = [&](auto kernel) {
         hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, stride,

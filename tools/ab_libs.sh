@@ -14,7 +14,11 @@ for rep in $(seq 1 $REPS); do
 import json, sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 r = d["roofline"]
-print(sys.argv[1].split("/")[-1], d["value"], r["avg_launch_ms"], r["frac"])
+line = [sys.argv[1].split("/")[-1], d["value"], r["avg_launch_ms"], r["frac"]]
+c = d.get("reas_cold")
+if c:
+    line += ["cold", c.get("value"), c.get("roofline", {}).get("avg_launch_ms"), c.get("roofline", {}).get("frac")]
+print(*line)
 PY
   done
 done

@@ -32,6 +32,10 @@ constexpr int kScatBlock = 256;             // scatter / pipelined scatter+class
 constexpr uint32_t kPollSleep = 1;          // s_sleep units (64 clocks) between table slot polls
 constexpr int kReasU = 4;                   // 16-byte chunks per thread per copy round (fused kernel)
 constexpr int kScatU = 4;                   // the same for the scatter forms
+// ... and for slots above 4 KiB: one 8976-byte datagram (561 chunks) fills 73 % of a
+// 768-chunk round instead of 55 % of 1024.  Config 3's split reassembly 210.6-212.7 ->
+// 207.7-208.9 us (profiles/round5/xcd_order/ab.log; 8 chunks, two datagrams a round: 215 us)
+constexpr int kScatUJumbo = 3;
 // fused kernel: run tails of events of at least this many bytes add to the event
 // accumulator after the copy, not during classification
 constexpr uint32_t kDeferAccBytes = 4194304u;
@@ -40,7 +44,6 @@ constexpr uint32_t kDeferAccBytes = 4194304u;
 // (launch_reas_scatter's nt; capi.cpp: E2SAR_HIP_REAS_COLD_DATAGRAMS, or a batch too large to
 // be cached).  Cold: a 205 x 1 MiB batch's scatter 85.1 (nt) vs 89.3 us (plain); hot: 68.0
 // (plain) vs 89.4 us (nt), reference-order batches 124.8 vs 148.1 us (profiles/round2/ab3/nt).
-constexpr uint32_t kScatterChunksPerBlock = 1024u;   // one round of 256 threads x 4 chunks
 constexpr uint32_t kReasChunksPerBlock = 9216u;      // fused group budget before balancing
 
 // Timeline trace (experiment builds only, -DE2SAR_TRACE=1): per workgroup, s_memrealtime
@@ -2151,16 +2154,17 @@ constexpr uint32_t kPipeClsAtPercent = 75;
 
 // Scatter workgroups of the launch: groups of G whole datagrams; returns G and the
 // workgroup count.
+__host__ __device__ constexpr int scatter_u(uint32_t stride) { return stride > 4096u ? kScatUJumbo : kScatU; }
 static uint32_t scatter_group_size(uint32_t stride)
 {
-    // datagrams per scatter workgroup: at most kScatterChunksPerBlock 16-byte chunks (one
-    // round of 256 threads x 4), <= 64.  The scatter needs no table round trip, so it
+    // datagrams per scatter workgroup: at most one round of 16-byte chunks (256 threads x
+    // scatter_u), <= 64.  The scatter needs no table round trip, so it
     // streams best in one-round workgroups, like seg_kernel: at 205 x 1 MiB, MTU 1500, a
     // batch read back cold takes 81.5 us with 1K-chunk groups against 100.3 us with the
     // fused kernel's 9K budget (89.5 us at 2K); hot, 68.7 us.
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > kScatterChunksPerBlock * (kScatBlock / kBlock)) G >>= 1;
+    while (G > 1 && G * spc > (uint32_t)(kScatBlock * scatter_u(stride))) G >>= 1;
     return G;
 }
 static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
@@ -2325,7 +2329,6 @@ static size_t scatter_lds(K kernel, bool stage, bool nt)
 hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t stride, uint32_t n,
                                const void *work, hipStream_t stream, bool nt)
 {
-    constexpr int U = kScatU;
     if (n == 0) return hipSuccess;
     const uint8_t *w = static_cast<const uint8_t *>(work);
     uint32_t blocks = 0;
@@ -2337,7 +2340,9 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
         hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, pkts, stride,
                            n, G, info, fin);
     };
-    if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
+    constexpr int U = kScatU, UJ = kScatUJumbo;
+    if (scatter_u(stride) == UJ) nt ? go(reas_scatter_kernel<UJ, true, true>) : go(reas_scatter_kernel<UJ, false, true>);
+    else if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
     else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
     return hipGetLastError();
 }
@@ -2346,7 +2351,6 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                                         const void *swork, const uint8_t *cpk, const uint32_t *clens, uint32_t cn,
                                         uint64_t now, void *cwork, hipStream_t stream, bool nt)
 {
-    constexpr int U = kScatU;
     if (cn == 0) return launch_reas_scatter(R, spk, stride, sn, swork, stream, nt);
     if (sn == 0) return launch_reas_classify(R, cpk, stride, clens, cn, now, cwork, stream);
     const uint8_t *sw = static_cast<const uint8_t *>(swork);
@@ -2370,7 +2374,10 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                            reinterpret_cast<PktInfo *>(cw), reinterpret_cast<FinishRec *>(cw + work_fin_off(cn)), nCls,
                            clsStart);
     };
-    if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
+    constexpr int U = kScatU, UJ = kScatUJumbo;
+    if (scatter_u(stride) == UJ)
+        nt ? go(reas_scatter_classify_kernel<UJ, true, true>) : go(reas_scatter_classify_kernel<UJ, false, true>);
+    else if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
     else st ? go(reas_scatter_classify_kernel<U, false, true>) : go(reas_scatter_classify_kernel<U, false, false>);
     return hipGetLastError();
 }

@@ -36,6 +36,7 @@ constexpr int kScatU = 4;                   // the same for the scatter forms
 // 768-chunk round instead of 55 % of 1024.  Config 3's split reassembly 210.6-212.7 ->
 // 207.7-208.9 us (profiles/round5/xcd_order/ab.log; 8 chunks, two datagrams a round: 215 us)
 constexpr int kScatUJumbo = 3;
+constexpr int kScatBlockJumbo = 256;        // scatter workgroup size for slots above 4 KiB
 // fused kernel: run tails of events of at least this many bytes add to the event
 // accumulator after the copy, not during classification
 constexpr uint32_t kDeferAccBytes = 4194304u;
@@ -1347,16 +1348,16 @@ __device__ __forceinline__ void classify_wave_to_work(const ReasDev &R, const ui
 // aligned: the loads need nothing from the work records, the stores are whole aligned
 // 16-byte stores except at the payload's two edges.  A payload that is not dword-congruent
 // with its destination (never at dword-multiple maxPld) is stored from registers as before.
-template <int U>
+template <int U, int TB>
 __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x4 (&x)[U], const uint32_t (&pp)[U],
                                                 const uint32_t (&cc)[U], uint32_t nch, uint32_t gn, uint32_t stride)
 {
     // one round of the group's slots (<= 256 * U chunks) plus 16 bytes of phase per datagram
-    __shared__ uint32_t stage[(16u * kScatBlock * U + 64u * 16u) / 4u];
+    __shared__ uint32_t stage[(16u * TB * U + 64u * 16u) / 4u];
     const uint32_t ps = stride + 16u;                                  // LDS bytes per datagram
 #pragma unroll
     for (int u = 0; u < U; u++) {
-        const uint32_t i = (uint32_t)u * kScatBlock + threadIdx.x;
+        const uint32_t i = (uint32_t)u * TB + threadIdx.x;
         if (i >= nch) continue;
         const PktInfo pi = sinfo[pp[u]];
         if (pi.plen == 0u) continue;
@@ -1375,7 +1376,7 @@ __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x
     lds_barrier();
     const uint32_t nbp = ps >> 4;                                      // 16-byte blocks per datagram
     const uint32_t total = gn * nbp;
-    for (uint32_t k = threadIdx.x; k < total; k += kScatBlock) {
+    for (uint32_t k = threadIdx.x; k < total; k += TB) {
         const uint32_t p = k / nbp, b = k - p * nbp;
         const PktInfo pi = sinfo[p];
         if (pi.plen == 0u) continue;
@@ -1399,7 +1400,7 @@ __device__ __forceinline__ void lds_stage_store(const PktInfo *sinfo, const u32x
 }
 
 // One workgroup: scatter datagrams [blk*G, blk*G+G) of a classified batch.
-template <int U, bool NT, bool STAGE>
+template <int U, bool NT, bool STAGE, int TB>
 __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                               uint32_t n, uint32_t G, const PktInfo *__restrict__ info,
                                               const FinishRec *__restrict__ fin, uint32_t blk, PktInfo *sinfo)
@@ -1421,7 +1422,7 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     auto issue = [&](uint32_t r0) {
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kScatBlock + threadIdx.x;
+            const uint32_t i = r0 + (uint32_t)u * TB + threadIdx.x;
             const uint32_t ic = (i < nch) ? i : 0u;
             uint32_t p = (uint32_t)((float)ic * rspc);
             if (p * spc > ic) p--;
@@ -1448,16 +1449,16 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
     __syncthreads();
 
     if constexpr (STAGE) {
-        if (nch <= (uint32_t)(kScatBlock * U)) {
-            lds_stage_store<U>(sinfo, x, pp, cc, nch, gn, stride);
+        if (nch <= (uint32_t)(TB * U)) {
+            lds_stage_store<U, TB>(sinfo, x, pp, cc, nch, gn, stride);
             nch = 0;                                                 // done: skip the rounds below
         }
     }
-    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(kScatBlock * U)) {
+    for (uint32_t r0 = 0; r0 < nch; r0 += (uint32_t)(TB * U)) {
         if (r0) issue(r0);
 #pragma unroll
         for (int u = 0; u < U; u++) {
-            const uint32_t i = r0 + (uint32_t)u * kScatBlock + threadIdx.x;
+            const uint32_t i = r0 + (uint32_t)u * TB + threadIdx.x;
             if (i >= nch) continue;
             scatter_chunk(sinfo[pp[u]], cc[u], x[u]);
         }
@@ -1504,21 +1505,21 @@ __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const 
     classify_wave_to_work(R, pkts, stride, lens, n, now, info, fin, blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6));
 }
 
-template <int U, bool NT, bool STAGE>
-__global__ __launch_bounds__(kScatBlock) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
+template <int U, bool NT, bool STAGE, int TB = kScatBlock>
+__global__ __launch_bounds__(TB) void reas_scatter_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t n, uint32_t G,
                                                               const PktInfo *__restrict__ info,
                                                               const FinishRec *__restrict__ fin)
 {
     __shared__ PktInfo sinfo[64];
-    scatter_group<U, NT, STAGE>(R, pkts, stride, n, G, info, fin, xcd_runs(blockIdx.x, (n + G - 1u) / G), sinfo);
+    scatter_group<U, NT, STAGE, TB>(R, pkts, stride, n, G, info, fin, xcd_runs(blockIdx.x, (n + G - 1u) / G), sinfo);
 }
 
 // Pipelined form: workgroups [clsStart, clsStart + nClsBlocks) classify batch b+1, the rest
 // scatter batch b (in xcd_runs order: clsStart and nClsBlocks are multiples of 8, so a
 // scatter workgroup's index keeps its XCD parity).
-template <int U, bool NT, bool STAGE>
-__global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
+template <int U, bool NT, bool STAGE, int TB = kScatBlock>
+__global__ __launch_bounds__(TB) void reas_scatter_classify_kernel(
     ReasDev R, uint32_t stride, const uint8_t *__restrict__ spk, uint32_t sn, uint32_t G,
     const PktInfo *__restrict__ sinfoG, const FinishRec *__restrict__ sfin, const uint8_t *__restrict__ cpk,
     const uint32_t *__restrict__ clens, uint32_t cn, uint64_t now, PktInfo *__restrict__ cinfo,
@@ -1529,11 +1530,11 @@ __global__ __launch_bounds__(kScatBlock) void reas_scatter_classify_kernel(
     const uint32_t b = blockIdx.x;
     if (b - clsStart < nClsBlocks) {
         classify_wave_to_work(R, cpk, stride, clens, cn, now, cinfo, cfin,
-                              (b - clsStart) * (kScatBlock / 64) + (threadIdx.x >> 6));
+                              (b - clsStart) * (TB / 64) + (threadIdx.x >> 6));
         return;
     }
     const uint32_t sb = (b < clsStart) ? b : b - nClsBlocks;
-    scatter_group<U, NT, STAGE>(R, spk, stride, sn, G, sinfoG, sfin, xcd_runs(sb, (sn + G - 1u) / G), sinfo);
+    scatter_group<U, NT, STAGE, TB>(R, spk, stride, sn, G, sinfoG, sfin, xcd_runs(sb, (sn + G - 1u) / G), sinfo);
 }
 
 // ---------------------------------------------------------------------------------
@@ -2155,6 +2156,7 @@ constexpr uint32_t kPipeClsAtPercent = 75;
 // Scatter workgroups of the launch: groups of G whole datagrams; returns G and the
 // workgroup count.
 __host__ __device__ constexpr int scatter_u(uint32_t stride) { return stride > 4096u ? kScatUJumbo : kScatU; }
+__host__ __device__ constexpr int scatter_tb(uint32_t stride) { return stride > 4096u ? kScatBlockJumbo : kScatBlock; }
 static uint32_t scatter_group_size(uint32_t stride)
 {
     // datagrams per scatter workgroup: at most one round of 16-byte chunks (256 threads x
@@ -2164,7 +2166,7 @@ static uint32_t scatter_group_size(uint32_t stride)
     // fused kernel's 9K budget (89.5 us at 2K); hot, 68.7 us.
     const uint32_t spc = stride >> 4;
     uint32_t G = 64;
-    while (G > 1 && G * spc > (uint32_t)(kScatBlock * scatter_u(stride))) G >>= 1;
+    while (G > 1 && G * spc > (uint32_t)(scatter_tb(stride) * scatter_u(stride))) G >>= 1;
     return G;
 }
 static uint32_t scatter_geometry(uint32_t stride, uint32_t n, uint32_t &blocks)
@@ -2337,11 +2339,12 @@ hipError_t launch_reas_scatter(const ReasDev &R, const uint8_t *pkts, uint32_t s
     const FinishRec *fin = reinterpret_cast<const FinishRec *>(w + work_fin_off(n));
     const bool st = scatter_stage(stride, nt);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, pkts, stride,
+        hipLaunchKernelGGL(kernel, dim3(blocks), dim3(scatter_tb(stride)), scatter_lds(kernel, st, nt), stream, R, pkts, stride,
                            n, G, info, fin);
     };
     constexpr int U = kScatU, UJ = kScatUJumbo;
-    if (scatter_u(stride) == UJ) nt ? go(reas_scatter_kernel<UJ, true, true>) : go(reas_scatter_kernel<UJ, false, true>);
+    constexpr int TJ = kScatBlockJumbo;
+    if (scatter_u(stride) == UJ) nt ? go(reas_scatter_kernel<UJ, true, true, TJ>) : go(reas_scatter_kernel<UJ, false, true, TJ>);
     else if (nt) st ? go(reas_scatter_kernel<U, true, true>) : go(reas_scatter_kernel<U, true, false>);
     else st ? go(reas_scatter_kernel<U, false, true>) : go(reas_scatter_kernel<U, false, false>);
     return hipGetLastError();
@@ -2357,7 +2360,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     uint8_t *cw = static_cast<uint8_t *>(cwork);
     uint32_t sblocks = 0;
     const uint32_t G = scatter_geometry(stride, sn, sblocks);
-    const uint32_t nCls = (cdiv(cn, kScatBlock) + 7u) & ~7u;     // multiples of 8: see xcd_runs
+    const uint32_t nCls = (cdiv(cn, (uint32_t)scatter_tb(stride)) + 7u) & ~7u;     // multiples of 8: see xcd_runs
     // where the classify workgroups sit in the grid: kPipeClsAtPercent of the way
     // through the scatter workgroups.  At the front (0, round 2's form) they hold ~590
     // workgroup slots through their dependent round trips while the scatter ramps up; three
@@ -2367,7 +2370,7 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
     const uint32_t clsStart = (uint32_t)((uint64_t)sblocks * kPipeClsAtPercent / 100u) & ~7u;
     const bool st = scatter_stage(stride, nt);
     auto go = [&](auto kernel) {
-        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(kScatBlock), scatter_lds(kernel, st, nt), stream, R, stride,
+        hipLaunchKernelGGL(kernel, dim3(nCls + sblocks), dim3(scatter_tb(stride)), scatter_lds(kernel, st, nt), stream, R, stride,
                            spk, sn, G,
                            reinterpret_cast<const PktInfo *>(sw),
                            reinterpret_cast<const FinishRec *>(sw + work_fin_off(sn)), cpk, clens, cn, now,
@@ -2375,8 +2378,9 @@ hipError_t launch_reas_scatter_classify(const ReasDev &R, uint32_t stride, const
                            clsStart);
     };
     constexpr int U = kScatU, UJ = kScatUJumbo;
+    constexpr int TJ = kScatBlockJumbo;
     if (scatter_u(stride) == UJ)
-        nt ? go(reas_scatter_classify_kernel<UJ, true, true>) : go(reas_scatter_classify_kernel<UJ, false, true>);
+        nt ? go(reas_scatter_classify_kernel<UJ, true, true, TJ>) : go(reas_scatter_classify_kernel<UJ, false, true, TJ>);
     else if (nt) st ? go(reas_scatter_classify_kernel<U, true, true>) : go(reas_scatter_classify_kernel<U, true, false>);
     else st ? go(reas_scatter_classify_kernel<U, false, true>) : go(reas_scatter_classify_kernel<U, false, false>);
     return hipGetLastError();

@@ -1489,13 +1489,27 @@ __device__ __forceinline__ void scatter_group(const ReasDev &R, const uint8_t *_
 // unchanged within noise (profiles/round5/xcd_order/).  A bijection on [0, nb): the last
 // nb mod (8 kXcdRun) groups keep their order.
 constexpr uint32_t kXcdRun = 128;
-__device__ __forceinline__ uint32_t xcd_runs(uint32_t b, uint32_t nb)
+__host__ __device__ constexpr uint32_t xcd_runs(uint32_t b, uint32_t nb)
 {
     constexpr uint32_t W = 8u * kXcdRun;
     if (b >= nb / W * W) return b;
     const uint32_t w = b % W;
     return (b - w) + (w % 8u) * kXcdRun + w / 8u;
 }
+// every group is visited exactly once (checked at compile time around the window edges)
+constexpr bool xcd_runs_bijective(uint32_t nb)
+{
+    bool seen[3200] = {};
+    for (uint32_t b = 0; b < nb; b++) {
+        const uint32_t g = xcd_runs(b, nb);
+        if (g >= nb || seen[g]) return false;
+        seen[g] = true;
+    }
+    return true;
+}
+static_assert(xcd_runs_bijective(1) && xcd_runs_bijective(1023) && xcd_runs_bijective(1024) &&
+                  xcd_runs_bijective(1025) && xcd_runs_bijective(2048) && xcd_runs_bijective(3199),
+              "xcd_runs must be a bijection on [0, nb)");
 
 __global__ __launch_bounds__(kBlock) void reas_classify_kernel(ReasDev R, const uint8_t *__restrict__ pkts,
                                                                uint32_t stride, const uint32_t *__restrict__ lens,

@@ -2,7 +2,8 @@
 """Copy the judged summaries of a GPU evidence pass (tools/profile_round4.sh, c3_bimodal.sh,
 the default bench line) from gpurun_out/ into profiles/round4/TAG/, and point the committed
 PMC summaries bench.py reads (profiles/pmc_*.json) at them.
-Usage: tools/collect_round4.py SRC_DIR TAG   (SRC_DIR e.g. gpurun_out/r4_gpu3)"""
+Usage: tools/collect_round4.py SRC_DIR TAG [ROUND]   (SRC_DIR e.g. gpurun_out/r4_gpu3; ROUND
+default round4: the summaries go to profiles/ROUND/TAG/)"""
 import csv
 import json
 import os
@@ -11,8 +12,9 @@ import statistics as st
 import sys
 
 src, tag = sys.argv[1], sys.argv[2]
+rnd = sys.argv[3] if len(sys.argv) > 3 else "round4"
 root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-dst = os.path.join(root, "profiles", "round4", tag)
+dst = os.path.join(root, "profiles", rnd, tag)
 os.makedirs(dst, exist_ok=True)
 for f in ("bench_default.json", "bench_n2_gloo.json"):
     if os.path.exists(os.path.join(src, f)):

@@ -749,6 +749,14 @@ def run_workload(args, env, headline: bool):
     def kernel_times(fn, steps):
         timing.clear()
         timing_on[0] = True
+        if not spread:
+            # keep the GPU behind the host for the whole pass: a spin kernel in front lets
+            # every launch and event pair be queued before the GPU reaches them, so a pair
+            # brackets GPU time only.  Without it, short eager launches (the cold leg's
+            # classify, recycle) drain the queue and the host's launch overhead for the next
+            # launch lands inside that launch's event pair: cold leg 82.3 us per launch by
+            # events against 78.5 us by rocprof, classify 23.3 against 12.4 (round 5).
+            torch.cuda._sleep(int(20e6) * max(1, steps))
         for _ in range(max(1, steps)):
             fn()
         torch.cuda.synchronize()

@@ -94,10 +94,12 @@ def parse(argv=None):
                     help="steps of the cold receive-only leg (0 = skip): reassembly of datagrams that were "
                          "written long before and are read back from HBM")
     ap.add_argument("--cold-batch-events", type=int, default=0,
-                    help="events per reassembly launch in the cold leg (0 = --batch-events); the cold leg "
-                         "does not depend on the Infinity Cache holding a batch, so larger launches only "
-                         "amortise a launch's head and tail")
-    ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="pipelined",
+                    help="events per reassembly launch in the cold leg (0 = every event of the step in one "
+                         "classify and one scatter launch); the cold leg does not depend on the Infinity "
+                         "Cache holding a batch, so larger launches only amortise a launch's head and tail "
+                         "(round 5: split form, 1024 / 512 / 205 events: 2552-2564 / 2471 / 2278-2293 GiB/s; "
+                         "pipelined 205 / 512: 2418-2444 / 2522-2527)")
+    ap.add_argument("--cold-reas", choices=["fused", "split", "pipelined"], default="split",
                     help="launch form of the cold leg (split: classify + scatter launches, timed apart; "
                          "pipelined: classify(0), then scatter(b) beside classify(b+1) in one launch)")
     ap.add_argument("--subs", default="auto",
@@ -833,7 +835,7 @@ def run_workload(args, env, headline: bool):
         R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                                   lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
                                   flags=_capi.REAS_COLD_DATAGRAMS)
-        cb = args.cold_batch_events or args.batch_events
+        cb = args.cold_batch_events or E
         cplans = plans if cb == args.batch_events else make_plans(cb)
         cbufs = [seg.alloc_packets(p.total_packets) for p in cplans]
         for p, (pk, ln) in zip(cplans, cbufs):
@@ -890,6 +892,9 @@ def run_workload(args, env, headline: bool):
                      "pipelined": "reas_classify_kernel(0), then reas_scatter_classify_kernel: scatter(b) "
                                   "beside classify(b+1)"}[args.cold_reas],
             "value": round(E * B * world * ck / cel / 2**30, 3), "unit": "GiB/s", "steps": ck,
+            # the whole leg (every launch: classify, scatter, recycle) against the same peak
+            "leg_achieved_GBps": round(E * (2 * B + 36 * npk) * ck / cel / 1e9, 1),
+            "leg_frac": round(E * (2 * B + 36 * npk) * ck / cel / 1e9 / HBM_PEAK_GBS, 4),
             "ms_per_step": round(cel / ck * 1e3, 4), "verified": cver,
             "roofline": {"bound": "hbm", "kernel": ckern, "achieved": round(c_ach, 1),
                          "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(c_ach / HBM_PEAK_GBS, 4),

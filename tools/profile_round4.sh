@@ -14,7 +14,7 @@ cd /tmp && export TMPDIR=/tmp
 for w in $W; do
   case $w in
     headline) A="--subs none --cold-steps 0"; P="$A"; WL="mtu=1500,event_bytes=1048576,batch_events=205,lb_version=2";;
-    cold)     A="--subs none --cold-steps 8"; P="--subs none --cold-steps 2"; WL="mtu=1500,event_bytes=1048576,batch_events=205,lb_version=2";;
+    cold)     A="--subs none --cold-steps 8"; P="--subs none --cold-steps 2"; WL="mtu=1500,event_bytes=1048576,batch_events=1024,lb_version=2";;
     mtu9000)  A="--subs none --cold-steps 0 --mtu 9000"; P="$A"; WL="mtu=9000,event_bytes=1048576,batch_events=205,lb_version=2";;
     config3)  A="--subs none --cold-steps 0 --mtu 9000 --event-bytes 8388608 --events 280 --batch-events 70"; P="$A"; WL="mtu=9000,event_bytes=8388608,batch_events=70,lb_version=2";;
   esac

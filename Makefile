@@ -5,7 +5,7 @@ HIPFLAGS ?= -O3 -std=c++17 -fPIC --offload-arch=$(ARCH) -Wall -Wno-unused-result
 INC := -Iinclude -Ie2sar_amd/csrc
 LIBDIR := e2sar_amd/lib
 
-HIP_SRCS := e2sar_amd/csrc/sar_kernels.hip e2sar_amd/csrc/ro_sort.hip e2sar_amd/csrc/capi.cpp
+HIP_SRCS := e2sar_amd/csrc/sar_kernels.hip e2sar_amd/csrc/capi.cpp
 HIP_HDRS := include/e2sar_hip.h e2sar_amd/csrc/sar_kernels.hpp e2sar_amd/csrc/wire.hpp
 
 all: $(LIBDIR)/libe2sar_hip.so oracle

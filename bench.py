@@ -942,8 +942,8 @@ def run_workload(args, env, headline: bool):
                 "lanes": args.lanes,
                 "xcd_groups": bool(groups and all(g[1] for g in groups)),
                 "reassembly": {"fused": ("reas_kernel per batch" if fused_name == "reas_kernel" else
-                                         "reassemble_batch per batch, REFERENCE_ORDER: key pass, radix sort, "
-                                         "per-key walk, scatter" if args.reference_order else
+                                         "reassemble_batch per batch, REFERENCE_ORDER: key pass (runs filed "
+                                         "per key), per-key walk, scatter" if args.reference_order else
                                          "reassemble_batch per batch: classify + scatter launches inside "
                                          "(batch above 320 MiB of slots)"),
                                "split": "reas_classify_kernel + reas_scatter_kernel per batch",

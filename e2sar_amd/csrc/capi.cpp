@@ -600,10 +600,13 @@ uint8_t *e2sar_hip_reas_arena(e2sar_hip_reas *r) { return r ? r->dev.arena : nul
 // Scratch of the reference-order classification for n datagrams on stream s (caller holds r->mu).
 static int ro_prepare(e2sar_hip_reas *r, hipStream_t s, uint32_t n)
 {
-    const size_t need = ro_scratch_bytes(n, r->dev.tableSlots);
-    if (need == 0) return fail(E2SAR_HIP_ERR_SYSTEM, "sort storage query failed");
+    // the run counters at the front are zero between batches (the kernels reset what they
+    // use); a new buffer starts them at zero
     auto &sc = r->scratch[s];
-    return grow(r, s, sc.roScratch, sc.roScratchBytes, need);
+    bool grew = false;
+    if (int rc = grow(r, s, sc.roScratch, sc.roScratchBytes, ro_scratch_bytes(n, r->dev.tableSlots), &grew)) return rc;
+    if (grew) HIP_TRY(hipMemsetAsync(sc.roScratch, 0, ro_zero_bytes(r->dev.tableSlots), s));
+    return E2SAR_HIP_OK;
 }
 
 extern "C" {
@@ -858,7 +861,9 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const ui
     hipError_t e;
     if (ref_order(r)) {
         // arrival order needs the classification of b+1 after that of b, not inside the
-        // scatter of b: two launches, same results
+        // scatter of b: two launches, same results.  (Round 5: the classification of b+1 on
+        // a side stream beside the scatter of b measured slower -- the scatter 63 -> 102-113
+        // us beside it, DESIGN.md 3 -- so the two run in line.)
         e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s, cold_loads(r, sn, stride));
         if (e == hipSuccess && cn) {
             if (int rc = ro_prepare(r, s, cn)) return rc;

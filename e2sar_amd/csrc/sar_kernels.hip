@@ -1563,13 +1563,16 @@ __global__ __launch_bounds__(TB) void reas_scatter_classify_kernel(
 // arrives after completion starts an item of its own.  This mode reproduces that for any
 // arrival order (batch order, then datagram order within a batch):
 //   ro_key_kernel  : parse and validate every datagram (counters as classify_wave), register
-//                    its key in the table (find_or_create<keyOnly>) and emit a sort key
-//                    slot << 32 | position and a 16-byte record {off, plen, blen, hl};
-//   ro_sort_keys   : rocPRIM radix sort of the keys (ro_sort.hip);
-//   ro_starts_kernel: the first sorted position of every key;
-//   ro_walk_kernel : one wave per key walks that key's datagrams in arrival order with the
-//                    reference's rules, creating items (arena buffers) as it goes, and writes
-//                    the PktInfo / FinishRec work records of the split form;
+//                    its key in the table (find_or_create<keyOnly>), write a 16-byte record
+//                    {off, plen, blen, hl}, and append every run of consecutive positions of
+//                    one key (per wave) as a RoRun, counted per slot;
+//   ro_place_kernel: one workgroup: the runs grouped by slot (a scan of the per-slot counts),
+//                    the list of keys that have runs, and the runs of any key with more than
+//                    64 of them sorted by position;
+//   ro_walk_kernel : one wave per key orders its runs by position (a wave sort of <= 64) and
+//                    walks that key's datagrams in arrival order with the reference's rules,
+//                    creating items (arena buffers) as it goes, and writes the PktInfo /
+//                    FinishRec work records of the split form;
 //   reas_scatter_kernel then moves the bytes and publishes the completions.
 
 // sort key of a datagram that does not take part (bad header, bounds, table full): slot
@@ -1578,10 +1581,8 @@ constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                                         const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
-                                                        unsigned long long *__restrict__ keys, RoRec *__restrict__ recs,
-                                                        uint32_t *__restrict__ nStarts)
+                                                        RoScratch sc, PktInfo *__restrict__ info)
 {
-    if (blockIdx.x == 0 && threadIdx.x == 0) *nStarts = 0u;     // counted by ro_starts_kernel
     const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t p0 = wave * 64u;
@@ -1615,36 +1616,153 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         h.derr = true;
     }
     if (live) {
-        keys[p] = ((unsigned long long)(h.ok ? slot : kRoNoSlot) << 32) | p;
         const u32x4 v = {h.off, h.pl, h.blen, hl};
-        st16(reinterpret_cast<uint8_t *>(recs + p), v);
+        st16(reinterpret_cast<uint8_t *>(sc.recs + p), v);
+        if (!h.ok) st16(reinterpret_cast<uint8_t *>(info + p), u32x4{0u, 0u, 0u, hl});   // takes no part
+    }
+    // runs of consecutive positions of one key (one slot) within the wave, filed in the
+    // slot's bucket (the first run of a slot in the batch lists the slot for the walk)
+    const uint32_t ks = h.ok ? slot : kRoNoSlot;
+    const uint32_t pks = lane_prev(ks, kRoNoSlot), nks = lane_next(ks, kRoNoSlot);
+    const bool rhead = h.ok && (lane == 0 || pks != ks);
+    const bool rtail = h.ok && (lane == 63 || nks != ks);
+    const uint64_t RT = __ballot(rtail);
+    if (rhead) {
+        const uint64_t below = (1ull << lane) - 1ull;
+        const uint32_t len = (uint32_t)__builtin_ctzll(RT & ~below) - lane + 1u;   // to this run's last lane
+        const uint32_t k = atomicAdd(&sc.runCnt[slot], 1u);
+        if (k == 0u) sc.active[atomicAdd(&sc.ctr[1], 1u)] = slot;
+        if (k < kRoBucket) {
+            sc.bucket[(size_t)slot * kRoBucket + k] = ((unsigned long long)p << 32) | len;
+        } else {
+            const uint32_t o = atomicAdd(&sc.ctr[0], 1u);
+            st16(reinterpret_cast<uint8_t *>(sc.runs + o), u32x4{slot, p, len, 0u});
+        }
     }
     wave_stats(R, live && !foreign, (live && !foreign) ? raw.len : 0u, h.bad, h.derr, wave);
 }
 
-// Key starts: the first sorted position of every key that takes part goes to starts[] (in
-// any order, counted in *nStarts); positions that take no part get their empty work
-// record here.
-__global__ __launch_bounds__(kBlock) void ro_starts_kernel(const unsigned long long *__restrict__ keys,
-                                                           const RoRec *__restrict__ recs, uint32_t n,
-                                                           uint32_t tableSlots, PktInfo *__restrict__ info,
-                                                           uint32_t *__restrict__ starts, uint32_t *__restrict__ nStarts)
+// One workgroup between the key pass and the walk: hands the count of listed keys to the walk
+// and resets the filing counters for the next batch.  Only when some key filed more than
+// kRoBucket runs (ctr[0] > 0 -- heavily reordered or very large events) does it do more: a
+// scan of those slots' run counts gives each its place, its bucket and its overflow runs are
+// copied there, and they are sorted by position (in LDS up to kRoSegLds runs, else a padded
+// bitonic sort in global memory).
+constexpr uint32_t kPlaceThreads = 1024, kRoSegLds = 8192;
+__device__ __forceinline__ void bitonic_lds(unsigned long long *v, uint32_t P)
 {
-    const uint32_t i = blockIdx.x * kBlock + threadIdx.x;
-    if (i >= n) return;
-    const unsigned long long k = keys[i];
-    const uint32_t slot = (uint32_t)(k >> 32);
-    if (slot >= tableSlots) {                                  // takes no part: nothing to copy
-        const uint32_t q = (uint32_t)k;
-        st16(reinterpret_cast<uint8_t *>(info + q), u32x4{0u, 0u, 0u, recs[q].hl});
-        return;
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += kPlaceThreads) {
+                const uint32_t q = i ^ j;
+                if (q > i) {
+                    const unsigned long long x = v[i], y = v[q];
+                    const bool up = (i & k) == 0u;
+                    if (up ? x > y : x < y) v[i] = y, v[q] = x;
+                }
+            }
+            __syncthreads();
+        }
+}
+__device__ __forceinline__ void bitonic_global(unsigned long long *v, uint32_t P)
+{
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += kPlaceThreads) {
+                const uint32_t q = i ^ j;
+                if (q > i) {
+                    const unsigned long long x = v[i], y = v[q];
+                    const bool up = (i & k) == 0u;
+                    if (up ? x > y : x < y) v[i] = y, v[q] = x;
+                }
+            }
+            __threadfence_block();
+            __syncthreads();
+        }
+}
+__global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, uint32_t T)
+{
+    __shared__ uint32_t part[kPlaceThreads];
+    __shared__ unsigned long long seg[kRoSegLds];
+    __shared__ uint32_t big[kPlaceThreads], nBig;
+    const uint32_t t = threadIdx.x;
+    const uint32_t nOver = sc.ctr[0];
+    if (t == 0) nBig = 0u;
+    __syncthreads();
+    if (t == 0) {
+        sc.ctr[2] = sc.ctr[1];
+        sc.ctr[1] = 0u;
+        sc.ctr[0] = 0u;
     }
-    if (i > 0 && (uint32_t)(keys[i - 1] >> 32) == slot) return;   // not the key's first position
-    starts[atomicAdd(nStarts, 1u)] = i;
+    if (nOver == 0u) return;                                          // uniform: the usual case
+    const uint32_t per = (T + kPlaceThreads - 1u) / kPlaceThreads;
+    const uint32_t s0 = t * per < T ? t * per : T, s1 = s0 + per < T ? s0 + per : T;
+    uint32_t sum = 0;
+    for (uint32_t q = s0; q < s1; q++) {
+        const uint32_t c = sc.runCnt[q];
+        sum += c > kRoBucket ? c : 0u;
+    }
+    part[t] = sum;
+    __syncthreads();
+    for (uint32_t off = 1; off < kPlaceThreads; off <<= 1) {           // inclusive scan
+        const uint32_t v = t >= off ? part[t - off] : 0u;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    uint32_t b = part[t] - sum;
+    for (uint32_t q = s0; q < s1; q++) {
+        const uint32_t c = sc.runCnt[q];
+        if (c <= kRoBucket) continue;
+        sc.runBase[q] = b;
+        sc.cursor[q] = b + kRoBucket;
+        for (uint32_t k = 0; k < kRoBucket; k++) sc.placed[b + k] = sc.bucket[(size_t)q * kRoBucket + k];
+        const uint32_t i = atomicAdd(&nBig, 1u);
+        if (i < kPlaceThreads) big[i] = q;
+        b += c;
+    }
+    __threadfence_block();
+    __syncthreads();
+    for (uint32_t r = t; r < nOver; r += kPlaceThreads) {
+        const RoRun run = sc.runs[r];
+        const uint32_t pos = atomicAdd(&sc.cursor[run.slot], 1u);
+        sc.placed[pos] = ((unsigned long long)run.start << 32) | run.len;
+    }
+    __threadfence_block();
+    __syncthreads();
+    // the LDS list holds up to kPlaceThreads slots; past that every slot is looked at
+    const bool over = nBig > kPlaceThreads;
+    const uint32_t nb = over ? T : nBig;
+    for (uint32_t i = 0; i < nb; i++) {
+        const uint32_t q = over ? i : big[i];
+        const uint32_t c = sc.runCnt[q];
+        if (c <= kRoBucket) continue;                                 // uniform over the workgroup
+        unsigned long long *g = sc.placed + sc.runBase[q];
+        uint32_t P = 1;
+        while (P < c) P <<= 1;
+        if (P <= kRoSegLds) {
+            for (uint32_t k = t; k < P; k += kPlaceThreads) seg[k] = k < c ? g[k] : ~0ull;
+            __syncthreads();
+            bitonic_lds(seg, P);
+            for (uint32_t k = t; k < c; k += kPlaceThreads) g[k] = seg[k];
+            __syncthreads();
+        } else {
+            for (uint32_t k = t; k < P; k += kPlaceThreads) sc.sortTmp[k] = k < c ? g[k] : ~0ull;
+            __threadfence_block();
+            __syncthreads();
+            bitonic_global(sc.sortTmp, P);
+            for (uint32_t k = t; k < c; k += kPlaceThreads) g[k] = sc.sortTmp[k];
+            __threadfence_block();
+            __syncthreads();
+        }
+    }
 }
 
 // One wave per key walks the key's datagrams in arrival order, 64 at a time, with the
-// reference's rules (cpp:361-427).  The item state (buffer, length, curBytes, fragments) is
+// reference's rules (cpp:361-427).  The key's runs are taken 64 at a time in position order --
+// a slot of at most kRoBucket runs sorts its bucket here by a bitonic wave sort, a larger one
+// was placed and sorted by ro_place_kernel -- and a datagram index of
+// the concatenated runs maps to its position by a binary search over the runs' prefix sums.  The item state (buffer, length, curBytes, fragments) is
 // wave-uniform.  Within a chunk the walk goes segment by segment: a segment starts where a
 // new item starts (offset 0, or no item in progress) and runs to the next offset-0 fragment;
 // a masked prefix sum of the payload lengths finds the first fragment whose add makes
@@ -1652,17 +1770,18 @@ __global__ __launch_bounds__(kBlock) void ro_starts_kernel(const unsigned long l
 // Fragments that overrun the item (made by a fragment with another bufferLength) count as
 // data errors and add nothing.  One segment per chunk is the usual case; duplicates, late
 // offset-0 fragments and replays after completion add segments.
-__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsigned long long *__restrict__ keys,
-                                                         const RoRec *__restrict__ recs, uint32_t n, uint64_t now,
-                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin,
-                                                         const uint32_t *__restrict__ starts,
-                                                         const uint32_t *__restrict__ nStarts)
+__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint64_t now,
+                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
 {
     const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    if (w >= *nStarts) return;                                 // wave-uniform
-    const uint32_t s = starts[w];
-    const uint32_t slot = (uint32_t)(keys[s] >> 32);
+    if (w >= sc.ctr[2]) return;                                // wave-uniform
+    const uint32_t slot = sc.active[w];
+    const uint32_t nRuns = sc.runCnt[slot];
+    const bool inBucket = nRuns <= kRoBucket;
+    const unsigned long long *__restrict__ runsOf =
+        inBucket ? sc.bucket + (size_t)slot * kRoBucket : sc.placed + sc.runBase[slot];
+    const RoRec *__restrict__ recs = sc.recs;
     ReasSlot *sl = R.slots + slot;
     const uint64_t ev = sl->eventNum;
     const uint32_t d = sl->dataId;
@@ -1674,21 +1793,48 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
     uint64_t created = sl->created;
     long long live = 0;                                        // net change of items in progress
     uint32_t derr = 0;
-    // the next chunk's sort keys are loaded while this chunk is walked (one dependent round
-    // trip per chunk -- its records -- instead of two)
-    unsigned long long kn = (s + lane < n) ? keys[s + lane] : ~0ull;
-    for (uint32_t base = s;; base += 64u) {
-        const unsigned long long kj = kn;
-        const bool valid = (uint32_t)(kj >> 32) == slot;     // the key's positions are contiguous
-        const uint32_t nv = (uint32_t)__builtin_popcountll(__ballot(valid));
-        if (nv == 0u) break;
-        const uint32_t q = (uint32_t)kj;
-        RoRec rc = {0u, 0u, 0u, 0u};
-        if (valid) rc = recs[q];
-        if (nv == 64u) {
-            const uint32_t jn = base + 64u + lane;
-            kn = (jn < n) ? keys[jn] : ~0ull;
+    for (uint32_t r0 = 0; r0 < nRuns; r0 += 64u) {
+    // this batch of the key's runs, in position order: start << 32 | length per lane
+    const uint32_t m = (nRuns - r0 < 64u) ? nRuns - r0 : 64u;
+    unsigned long long rv = (lane < m) ? runsOf[r0 + lane] : ~0ull;
+    if (inBucket) {                                            // bitonic wave sort (wave-uniform branch)
+#pragma unroll
+        for (uint32_t k = 2; k <= 64u; k <<= 1)
+#pragma unroll
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                const unsigned long long o = shfl_u64(rv, (int)(lane ^ j));
+                const bool lower = (lane & j) == 0u, up = (lane & k) == 0u;
+                if (lower == up ? o < rv : o > rv) rv = o;
+            }
+    }
+    const uint32_t rlen = (uint32_t)rv & 0xFFFFFFFFu, rstart = (uint32_t)(rv >> 32);
+    const uint32_t rl = lane < m ? rlen : 0u;
+    const uint32_t rin = wave_incl_scan(rl), rex = rin - rl;
+    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)rin, 63);
+    // position of datagram g of this batch of runs: in the last run whose prefix is <= g
+    auto pos_of = [&](uint32_t g) -> uint32_t {
+        uint32_t ri = 0;
+#pragma unroll
+        for (uint32_t step = 32; step; step >>= 1) {
+            const uint32_t c = ri + step;
+            const uint32_t ce = (uint32_t)__shfl((int)rex, (int)c);
+            if (c < m && ce <= g) ri = c;
         }
+        return (uint32_t)__shfl((int)rstart, (int)ri) + (g - (uint32_t)__shfl((int)rex, (int)ri));
+    };
+    // the next chunk's records are loaded while this chunk is walked
+    uint32_t qn = pos_of(lane);
+    RoRec rn = {0u, 0u, 0u, 0u};
+    if (lane < tot) rn = recs[qn];
+    for (uint32_t base = 0; base < tot; base += 64u) {
+        const bool valid = base + lane < tot;
+        const uint32_t q = qn;
+        const RoRec rc = rn;
+        if (base + 64u < tot) {
+            qn = pos_of(base + 64u + lane);
+            if (base + 64u + lane < tot) rn = recs[qn];
+        }
+        const uint32_t nv = (tot - base < 64u) ? tot - base : 64u;
         for (uint32_t t = 0; t < nv;) {
             if (!item || __shfl(rc.off, (int)t) == 0u) {
                 // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the
@@ -1745,9 +1891,10 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, const unsign
             if (cm) item = false;                              // inProgress-- in complete_event
             t = end;
         }
-        if (nv < 64u) break;
+    }
     }
     if (lane == 0) {
+        sc.runCnt[slot] = 0u;                                  // next batch
         if (item) {
             sl->bufOff = boff;
             sl->bytes = ibytes;
@@ -2405,21 +2552,17 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
                               hipStream_t stream)
 {
     if (n == 0) return hipSuccess;
-    uint8_t *w = static_cast<uint8_t *>(work);
-    RoScratch sc = ro_scratch_layout(scratch, n);
     if (ro_scratch_bytes(n, R.tableSlots) > scratchBytes) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
-                       sc.keysIn, sc.recs, sc.nStarts);
-    size_t tb = scratchBytes - (size_t)(sc.temp - static_cast<uint8_t *>(scratch));
-    hipError_t e = ro_sort_keys(sc.temp, tb, sc.keysIn, sc.keysOut, n, ro_sort_end_bit(R.tableSlots), stream);
-    if (e != hipSuccess) return e;
+    uint8_t *w = static_cast<uint8_t *>(work);
     PktInfo *info = reinterpret_cast<PktInfo *>(w);
-    hipLaunchKernelGGL(ro_starts_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, sc.keysOut, sc.recs, n,
-                       R.tableSlots, info, sc.starts, sc.nStarts);
+    const RoScratch sc = ro_scratch_layout(scratch, n, R.tableSlots);
+    hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
+                       sc, info);
+    hipLaunchKernelGGL(ro_place_kernel, dim3(1), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
-    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc.keysOut, sc.recs,
-                       n, now, info, reinterpret_cast<FinishRec *>(w + work_fin_off(n)), sc.starts, sc.nStarts);
+    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, now, info,
+                       reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }
 

@@ -130,43 +130,63 @@ static_assert(sizeof(FinishRec) == 32, "two dwordx4 per record");
 inline size_t work_fin_off(uint32_t n) { return ((size_t)n * sizeof(PktInfo) + 255) & ~(size_t)255; }
 inline size_t work_bytes(uint32_t n) { return work_fin_off(n) + (size_t)n * sizeof(FinishRec); }
 
-// Reference-order mode: per-datagram record of ro_key_kernel, and the scratch it needs
-// (sort keys in and out, records, rocPRIM temporary storage) for a batch of n datagrams.
+// Reference-order mode: per-datagram record of ro_key_kernel, and the scratch it needs for a
+// batch of n datagrams and a table of T slots.  Round 5: no sort of the datagrams -- the key
+// pass files every run of consecutive positions of one key into its slot's bucket of
+// kRoBucket runs (past that into an overflow list, placed and sorted by ro_place_kernel), and
+// each key's walk orders its own runs by position.
+constexpr uint32_t kRoBucket = 64;
 struct RoRec {
     uint32_t off, plen, blen, hl;
 };
 static_assert(sizeof(RoRec) == 16, "one dwordx4 per datagram");
+struct RoRun {
+    uint32_t slot, start, len, pad;
+};
+static_assert(sizeof(RoRun) == 16, "one dwordx4 per run");
 struct RoScratch {
-    unsigned long long *keysIn, *keysOut;
-    RoRec *recs;
-    uint32_t *starts, *nStarts;     // first sorted position of every key, and their count
-    uint8_t *temp;
+    uint32_t *ctr;                  // [0] overflow runs, [1] keys with runs (both zero between batches),
+                                    // [2] keys with runs for the walk
+    uint32_t *runCnt;               // [T] runs per slot                        (zero between batches)
+    uint32_t *runBase;              // [T] first placed run of a slot of more than kRoBucket runs
+    uint32_t *cursor;               // [T] placement cursor
+    uint32_t *active;               // [T] slots with runs in this batch
+    unsigned long long *bucket;     // [T][kRoBucket] start << 32 | len, in filing order
+    RoRec *recs;                    // [n]
+    RoRun *runs;                    // [n] overflow runs
+    unsigned long long *placed;     // [n] runs of the slots of more than kRoBucket runs, in position order
+    unsigned long long *sortTmp;    // [2n] padded sort of a slot's runs (only for slots of > 8192 runs)
 };
 inline size_t ro_align(size_t x) { return (x + 255) & ~(size_t)255; }
-inline size_t ro_fixed_bytes(uint32_t n) { return 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(4ull * n) + 256; }
-inline RoScratch ro_scratch_layout(void *base, uint32_t n)
+// the scratch's first bytes that must be zero before its first batch (later batches leave them zero)
+inline size_t ro_zero_bytes(uint32_t T) { return 256 + ro_align(4ull * T); }
+inline size_t ro_scratch_bytes(uint32_t n, uint32_t T)
+{
+    return ro_zero_bytes(T) + 3 * ro_align(4ull * T) + ro_align(8ull * kRoBucket * T) + ro_align(16ull * n) +
+           ro_align(16ull * n) + ro_align(8ull * n) + ro_align(16ull * n);
+}
+inline RoScratch ro_scratch_layout(void *base, uint32_t n, uint32_t T)
 {
     uint8_t *b = static_cast<uint8_t *>(base);
     RoScratch s;
-    s.keysIn = reinterpret_cast<unsigned long long *>(b);
-    s.keysOut = reinterpret_cast<unsigned long long *>(b + ro_align(8ull * n));
-    s.recs = reinterpret_cast<RoRec *>(b + 2 * ro_align(8ull * n));
-    s.starts = reinterpret_cast<uint32_t *>(b + 2 * ro_align(8ull * n) + ro_align(16ull * n));
-    s.nStarts = reinterpret_cast<uint32_t *>(b + 2 * ro_align(8ull * n) + ro_align(16ull * n) + ro_align(4ull * n));
-    s.temp = b + ro_fixed_bytes(n);
+    s.ctr = reinterpret_cast<uint32_t *>(b);
+    s.runCnt = reinterpret_cast<uint32_t *>(b + 256);
+    b += ro_zero_bytes(T);
+    s.runBase = reinterpret_cast<uint32_t *>(b);
+    s.cursor = reinterpret_cast<uint32_t *>(b + ro_align(4ull * T));
+    s.active = reinterpret_cast<uint32_t *>(b + 2 * ro_align(4ull * T));
+    b += 3 * ro_align(4ull * T);
+    s.bucket = reinterpret_cast<unsigned long long *>(b);
+    b += ro_align(8ull * kRoBucket * T);
+    s.recs = reinterpret_cast<RoRec *>(b);
+    b += ro_align(16ull * n);
+    s.runs = reinterpret_cast<RoRun *>(b);
+    b += ro_align(16ull * n);
+    s.placed = reinterpret_cast<unsigned long long *>(b);
+    b += ro_align(8ull * n);
+    s.sortTmp = reinterpret_cast<unsigned long long *>(b);
     return s;
 }
-// sort bits: slot (< tableSlots = 2^t) above the 32-bit position, plus the all-ones "no
-// slot" marker's bit t
-inline unsigned ro_sort_end_bit(uint32_t tableSlots)
-{
-    unsigned t = 0;
-    while ((1u << t) < tableSlots) t++;
-    return 33u + t;
-}
-hipError_t ro_sort_keys(void *temp, size_t &tempBytes, const unsigned long long *in, unsigned long long *out,
-                        uint32_t n, unsigned endBit, hipStream_t stream);   // temp == nullptr: size query
-size_t ro_scratch_bytes(uint32_t n, uint32_t tableSlots);
 hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,
                               uint32_t n, uint64_t now, void *work, void *scratch, size_t scratchBytes,
                               hipStream_t stream);

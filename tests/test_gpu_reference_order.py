@@ -193,8 +193,11 @@ def test_random_arrival_orders_match_the_reference(hip, seed):
     assert lost == rlost and loss == rloss and inp == rinp == 0
 
 
-def test_large_events_shuffled_with_duplicates(hip):
-    # 1 MiB events at MTU 1500, tails shuffled, a few duplicates and one late offset 0
+@pytest.mark.parametrize("mode", ["fused", "pipelined"])
+def test_large_events_shuffled_with_duplicates(hip, mode):
+    # 1 MiB events at MTU 1500, tails shuffled, a few duplicates and one late offset 0: every
+    # key files far more than kRoBucket runs per batch (the overflow placement and sort of
+    # ro_place_kernel); pipelined: each batch's key pass + walk beside the previous scatter
     rnd = random.Random(77)
     mp = O.max_pld_len(1500)
     stride = (36 + mp + 15) // 16 * 16
@@ -214,7 +217,8 @@ def test_large_events_shuffled_with_duplicates(hip):
     pk = np.stack([p for p, _ in out])
     ln = np.array([L for _, L in out], np.uint32)
     ref, rst, rlost, rloss, rinp = _oracle(pk, ln)
-    got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, len(ln) // 3, len(ln)], "fused")
+    n = len(ln)
+    got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, n // 3, n // 2, 5 * n // 6, n], mode)
     assert st == rst and sorted(got) == sorted(ref)
     for k in ref:
         assert sorted(got[k]) == sorted(ref[k])              # bytes and numFragments
@@ -222,10 +226,10 @@ def test_large_events_shuffled_with_duplicates(hip):
 
 
 def test_reference_order_in_a_replayed_graph(hip):
-    """Reference-order launches captured in a HIP graph and replayed: the sort inside must be
-    one a graph can hold (the slot sort has no memset node; rocPRIM's onesweep form, whose
-    look-back memset breaks replays, is never captured -- DESIGN.md 4.4), and every replay
-    gives the oracle's events."""
+    """Reference-order launches captured in a HIP graph and replayed: the key pass's run
+    filing holds no memset node (its counters are reset by the kernels that use them, a
+    captured hipMemsetAsync breaks replays -- DESIGN.md 4.4), and every replay gives the
+    oracle's events."""
     import torch
     from e2sar_amd import sar
 

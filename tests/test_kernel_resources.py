@@ -13,7 +13,7 @@ import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 HIPCC = "/opt/rocm/bin/hipcc"
-SOURCES = ["e2sar_amd/csrc/sar_kernels.hip", "e2sar_amd/csrc/ro_sort.hip"]
+SOURCES = ["e2sar_amd/csrc/sar_kernels.hip"]
 
 
 def _remarks(src, tmp_path):

@@ -10,5 +10,5 @@ rm -rf $D && mkdir -p $D && cp e2sar_amd/csrc/*.hip e2sar_amd/csrc/*.hpp e2sar_a
 for e in "$@"; do sed -i -e "$e" $D/sar_kernels.hip; done
 if cmp -s $D/sar_kernels.hip e2sar_amd/csrc/sar_kernels.hip; then echo "variant $N: no change"; exit 1; fi
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -I$D -shared \
-  -o build/variants/lib_$N.so $D/sar_kernels.hip $D/ro_sort.hip $D/capi.cpp
+  -o build/variants/lib_$N.so $D/sar_kernels.hip $D/capi.cpp
 echo "built build/variants/lib_$N.so"

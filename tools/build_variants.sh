@@ -4,7 +4,7 @@
 set -e
 mkdir -p build/variants
 H="/opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Iinclude -Ie2sar_amd/csrc -shared"
-S="e2sar_amd/csrc/sar_kernels.hip e2sar_amd/csrc/ro_sort.hip e2sar_amd/csrc/capi.cpp"
+S="e2sar_amd/csrc/sar_kernels.hip e2sar_amd/csrc/capi.cpp"
 while [ $# -gt 1 ]; do
   $H $2 -o build/variants/lib_$1.so $S &
   shift 2

@@ -107,7 +107,7 @@ sub("""    __shared__ ReasGroupLds L;
 open(p, "w").write(s)
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Iinclude", "-I" + dst,
        "-shared", "-o", os.path.join(root, "build/variants/lib_%s.so" % name),
-       p, os.path.join(dst, "ro_sort.hip"), os.path.join(dst, "capi.cpp")]
+       p, os.path.join(dst, "capi.cpp")]
 subprocess.run(cmd, check=True, cwd=root)
 r = subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "--offload-arch=gfx950", "--offload-device-only",
                     "-Iinclude", "-I" + dst, "-c", p, "-o", "/tmp/_v.o", "-Rpass-analysis=kernel-resource-usage"],

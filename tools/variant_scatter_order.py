@@ -36,6 +36,6 @@ s = s.replace(old, new)
 open(p, "w").write(s)
 cmd = ["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-fPIC", "--offload-arch=gfx950", "-Iinclude", "-I" + dst,
        "-shared", "-o", os.path.join(root, "build/variants/lib_%s.so" % name),
-       p, os.path.join(dst, "ro_sort.hip"), os.path.join(dst, "capi.cpp")]
+       p, os.path.join(dst, "capi.cpp")]
 subprocess.run(cmd, check=True, cwd=root)
 print("built lib_%s.so" % name)

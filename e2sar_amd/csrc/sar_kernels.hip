@@ -1648,7 +1648,7 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
 // scan of those slots' run counts gives each its place, its bucket and its overflow runs are
 // copied there, and they are sorted by position (in LDS up to kRoSegLds runs, else a padded
 // bitonic sort in global memory).
-constexpr uint32_t kPlaceThreads = 1024, kRoSegLds = 8192;
+constexpr uint32_t kPlaceThreads = 256, kRoSegLds = 2048;
 __device__ __forceinline__ void bitonic_lds(unsigned long long *v, uint32_t P)
 {
     for (uint32_t k = 2; k <= P; k <<= 1)
@@ -1760,8 +1760,8 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
 
 // One wave per key walks the key's datagrams in arrival order, 64 at a time, with the
 // reference's rules (cpp:361-427).  The key's runs are taken 64 at a time in position order --
-// a slot of at most kRoBucket runs sorts its bucket here by a bitonic wave sort, a larger one
-// was placed and sorted by ro_place_kernel -- and a datagram index of
+// a slot of at most kRoBucket runs orders its bucket here (rank by start, one lane push), a
+// larger one was placed and sorted by ro_place_kernel -- and a datagram index of
 // the concatenated runs maps to its position by a binary search over the runs' prefix sums.  The item state (buffer, length, curBytes, fragments) is
 // wave-uniform.  Within a chunk the walk goes segment by segment: a segment starts where a
 // new item starts (offset 0, or no item in progress) and runs to the next offset-0 fragment;
@@ -1770,17 +1770,21 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
 // Fragments that overrun the item (made by a fragment with another bufferLength) count as
 // data errors and add nothing.  One segment per chunk is the usual case; duplicates, late
 // offset-0 fragments and replays after completion add segments.
-__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint64_t now,
+constexpr uint32_t kRoAhead = 4;
+__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint32_t T, uint64_t now,
                                                          PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
 {
     const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
-    if (w >= sc.ctr[2]) return;                                // wave-uniform
-    const uint32_t slot = sc.active[w];
+    // the chain of dependent loads before the walk proper is kept short: the key is read
+    // beside the count of keys, and its bucket beside its run count
+    const uint32_t nKeys = sc.ctr[2];
+    const uint32_t slot = w < T ? sc.active[w] : 0u;
+    if (w >= nKeys) return;                                    // wave-uniform
     const uint32_t nRuns = sc.runCnt[slot];
+    const unsigned long long bv = sc.bucket[(size_t)slot * kRoBucket + lane];
     const bool inBucket = nRuns <= kRoBucket;
-    const unsigned long long *__restrict__ runsOf =
-        inBucket ? sc.bucket + (size_t)slot * kRoBucket : sc.placed + sc.runBase[slot];
+    const unsigned long long *__restrict__ runsOf = inBucket ? nullptr : sc.placed + sc.runBase[slot];
     const RoRec *__restrict__ recs = sc.recs;
     ReasSlot *sl = R.slots + slot;
     const uint64_t ev = sl->eventNum;
@@ -1796,55 +1800,52 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     for (uint32_t r0 = 0; r0 < nRuns; r0 += 64u) {
     // this batch of the key's runs, in position order: start << 32 | length per lane
     const uint32_t m = (nRuns - r0 < 64u) ? nRuns - r0 : 64u;
-    unsigned long long rv = (lane < m) ? runsOf[r0 + lane] : ~0ull;
-    if (inBucket) {                                            // bitonic wave sort (wave-uniform branch)
-#pragma unroll
-        for (uint32_t k = 2; k <= 64u; k <<= 1)
-#pragma unroll
-            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-                const unsigned long long o = shfl_u64(rv, (int)(lane ^ j));
-                const bool lower = (lane & j) == 0u, up = (lane & k) == 0u;
-                if (lower == up ? o < rv : o > rv) rv = o;
-            }
+    unsigned long long rv = (lane < m) ? (inBucket ? bv : runsOf[r0 + lane]) : ~0ull;
+    if (inBucket) {
+        // order the bucket by start (the starts are distinct): each run's rank is the number
+        // of runs that start before it (m scalar reads), then one push per word to lane rank
+        const uint32_t mys = (uint32_t)(rv >> 32);
+        uint32_t rank = 0;
+        for (uint32_t r = 0; r < m; r++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mys, (int)r) < mys ? 1u : 0u;
+        if (lane >= m) rank = lane;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)(uint32_t)rv);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)mys);
+        rv = ((unsigned long long)hi << 32) | lo;
     }
     const uint32_t rlen = (uint32_t)rv & 0xFFFFFFFFu, rstart = (uint32_t)(rv >> 32);
     const uint32_t rl = lane < m ? rlen : 0u;
     const uint32_t rin = wave_incl_scan(rl), rex = rin - rl;
     const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)rin, 63);
-    // position of datagram g of this batch of runs: in the last run whose prefix is <= g
-    auto pos_of = [&](uint32_t g) -> uint32_t {
-        uint32_t ri = 0;
-#pragma unroll
-        for (uint32_t step = 32; step; step >>= 1) {
-            const uint32_t c = ri + step;
-            const uint32_t ce = (uint32_t)__shfl((int)rex, (int)c);
-            if (c < m && ce <= g) ri = c;
+    // position of datagram base + lane of this batch of runs: in the last run whose prefix
+    // is <= it.  The runs that meet the chunk [base, base + 64) are r0..r1 (usually two): a
+    // uniform loop over them with scalar reads, no per-lane search
+    auto pos_of = [&](uint32_t base) -> uint32_t {
+        const uint32_t g = base + lane;
+        const uint64_t b0 = __ballot(lane < m && rex <= base), b1 = __ballot(lane < m && rex < base + 64u);
+        const int r0 = b0 ? 63 - __builtin_clzll(b0) : 0, r1 = b1 ? 63 - __builtin_clzll(b1) : 0;
+        uint32_t qb = 0;
+        for (int r = r0; r <= r1; r++) {
+            const uint32_t sr = (uint32_t)__builtin_amdgcn_readlane((int)rex, r);
+            const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)rstart, r);
+            if (g >= sr) qb = st - sr;
         }
-        return (uint32_t)__shfl((int)rstart, (int)ri) + (g - (uint32_t)__shfl((int)rex, (int)ri));
+        return qb + g;
     };
-    // the next chunk's records are loaded while this chunk is walked
-    uint32_t qn = pos_of(lane);
-    RoRec rn = {0u, 0u, 0u, 0u};
-    if (lane < tot) rn = recs[qn];
-    for (uint32_t base = 0; base < tot; base += 64u) {
+    // one chunk of 64 datagrams of the key, in arrival order (q: position, rc: record)
+    auto walk_chunk = [&](uint32_t base, uint32_t q, const RoRec &rc) {
         const bool valid = base + lane < tot;
-        const uint32_t q = qn;
-        const RoRec rc = rn;
-        if (base + 64u < tot) {
-            qn = pos_of(base + 64u + lane);
-            if (base + 64u + lane < tot) rn = recs[qn];
-        }
         const uint32_t nv = (tot - base < 64u) ? tot - base : 64u;
         for (uint32_t t = 0; t < nv;) {
-            if (!item || __shfl(rc.off, (int)t) == 0u) {
+            if (!item || (uint32_t)__builtin_amdgcn_readlane((int)rc.off, (int)t) == 0u) {
                 // a new item (EventQueueItem(rehdr), hpp:89-98); at offset 0 it replaces the
                 // one in progress (cpp:361-369), dropped without a lost record
                 if (item) live--;
-                const uint32_t blen = __shfl(rc.blen, (int)t);
+                const uint32_t blen = (uint32_t)__builtin_amdgcn_readlane((int)rc.blen, (int)t);
                 const uint64_t need = ((uint64_t)blen + 255ull) & ~255ull;
                 uint64_t nb = 0;
                 if (lane == 0) nb = atomicAdd(&R.ctl->arenaTop, (unsigned long long)(need ? need : 256ull));
-                nb = shfl_u64(nb, 0);
+                nb = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(nb >> 32), 0) << 32) |
+                     (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)nb, 0);
                 if (nb + blen > R.arenaBytes) {
                     if (lane == 0) atomicOr(&R.ctl->errorFlags, 2u);
                     nb = kNoBuf;
@@ -1890,6 +1891,34 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
             }
             if (cm) item = false;                              // inProgress-- in complete_event
             t = end;
+        }
+    };
+    // the records of the next kRoAhead - 1 chunks are in flight while a chunk is walked (the
+    // walk is a chain of dependent chunks over few waves: latency, not bandwidth, bounds it).
+    // The ring is indexed statically (unrolled by kRoAhead); a chunk's slot is reloaded after
+    // the chunk is walked.  (Round 5: staging a key's records in LDS by LDS-DMA, 16 chunks per
+    // wait, measured 16.6 against this ring's 15.5 us per launch: the chunks' own work, ~0.8
+    // us each at one wave per CU, not their loads, bounds the walk)
+    uint32_t qr[kRoAhead];
+    RoRec rr[kRoAhead];
+#pragma unroll
+    for (uint32_t i = 0; i < kRoAhead; i++) {
+        qr[i] = pos_of(i * 64u);
+        rr[i] = RoRec{0u, 0u, 0u, 0u};
+        if (i * 64u + lane < tot) rr[i] = recs[qr[i]];
+    }
+    for (uint32_t b0 = 0; b0 < tot; b0 += kRoAhead * 64u) {
+#pragma unroll
+        for (uint32_t i = 0; i < kRoAhead; i++) {
+            const uint32_t base = b0 + i * 64u;
+            if (base < tot) {                                  // wave-uniform
+                walk_chunk(base, qr[i], rr[i]);
+                const uint32_t nxt = base + kRoAhead * 64u;
+                if (nxt < tot) {
+                    qr[i] = pos_of(nxt);
+                    if (nxt + lane < tot) rr[i] = recs[qr[i]];
+                }
+            }
         }
     }
     }
@@ -2561,7 +2590,7 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     hipLaunchKernelGGL(ro_place_kernel, dim3(1), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
-    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, now, info,
+    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, R.tableSlots, now, info,
                        reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }

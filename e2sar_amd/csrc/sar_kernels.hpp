@@ -155,7 +155,7 @@ struct RoScratch {
     RoRec *recs;                    // [n]
     RoRun *runs;                    // [n] overflow runs
     unsigned long long *placed;     // [n] runs of the slots of more than kRoBucket runs, in position order
-    unsigned long long *sortTmp;    // [2n] padded sort of a slot's runs (only for slots of > 8192 runs)
+    unsigned long long *sortTmp;    // [2n] padded sort of a slot's runs (only for slots of > 2048 runs)
 };
 inline size_t ro_align(size_t x) { return (x + 255) & ~(size_t)255; }
 // the scratch's first bytes that must be zero before its first batch (later batches leave them zero)

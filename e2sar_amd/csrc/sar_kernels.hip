@@ -1564,19 +1564,20 @@ __global__ __launch_bounds__(TB) void reas_scatter_classify_kernel(
 // arrival order (batch order, then datagram order within a batch):
 //   ro_key_kernel  : parse and validate every datagram (counters as classify_wave), register
 //                    its key in the table (find_or_create<keyOnly>), write a 16-byte record
-//                    {off, plen, blen, hl}, and append every run of consecutive positions of
-//                    one key (per wave) as a RoRun, counted per slot;
-//   ro_place_kernel: one workgroup: the runs grouped by slot (a scan of the per-slot counts),
-//                    the list of keys that have runs, and the runs of any key with more than
-//                    64 of them sorted by position;
-//   ro_walk_kernel : one wave per key orders its runs by position (a wave sort of <= 64) and
+//                    {off, plen, blen, hl}, and file every run of consecutive positions of
+//                    one key (per wave) in the key's bucket of kRoBucket runs (past that in
+//                    an overflow list); a key's first run lists the key;
+//   ro_place_kernel: one workgroup: hands the number of listed keys to the walk and resets
+//                    the counters; only if a key overflowed its bucket, places and sorts by
+//                    position the runs of every such key;
+//   ro_walk_kernel : one wave per key orders its runs by position (rank and push, <= 64 runs) and
 //                    walks that key's datagrams in arrival order with the reference's rules,
 //                    creating items (arena buffers) as it goes, and writes the PktInfo /
 //                    FinishRec work records of the split form;
 //   reas_scatter_kernel then moves the bytes and publishes the completions.
 
-// sort key of a datagram that does not take part (bad header, bounds, table full): slot
-// field all ones, above every real slot, so those keys sort last
+// key of a datagram that does not take part (bad header, bounds, table full): no real slot,
+// so it joins no run
 constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
 
 __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,

@@ -1602,16 +1602,35 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         h.ok = false;
         h.derr = true;
     }
-    // runs of equal keys: only the run head registers the key
+    // runs of equal keys: only the run head takes part; of the run heads of one key in the
+    // wave (events interleaved in arrival make many), only the first registers the key and
+    // files the wave's runs of that key with one atomic.  The loop visits each distinct key
+    // of the wave once (usually one or two)
     const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(h.ev >> 32), 0u) << 32) | lane_prev((uint32_t)h.ev, 0u);
     const uint32_t pd = lane_prev(h.d, 0u), pok = lane_prev(h.ok ? 1u : 0u, 0u);
     const bool head = h.ok && (lane == 0 || !pok || pev != h.ev || pd != h.d);
-    const LookupResult lr = find_or_create<true>(R, head, h.ev, h.d, h.blen, now);
+    uint64_t same = 0;                                         // heads of this lane's key
+    uint32_t lead = lane;                                      // the first of them
+    for (uint64_t pend = __ballot(head); pend;) {              // wave-uniform
+        const uint32_t f = (uint32_t)__builtin_ctzll(pend);
+        const uint64_t fev = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(h.ev >> 32), (int)f) << 32) |
+                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h.ev, (int)f);
+        const uint32_t fd = (uint32_t)__builtin_amdgcn_readlane((int)h.d, (int)f);
+        const uint64_t m = __ballot(head && h.ev == fev && h.d == fd);
+        if ((m >> lane) & 1ull) {
+            same = m;
+            lead = f;
+        }
+        pend &= ~m;
+    }
+    const bool leader = head && lead == lane;
+    const LookupResult lr = find_or_create<true>(R, leader, h.ev, h.d, h.blen, now);
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const uint64_t hm = H & le;
     const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
-    const uint32_t slot = __shfl(lr.slot, myhead);
+    const uint32_t keyLead = __shfl(lead, myhead);
+    const uint32_t slot = __shfl(lr.slot, (int)keyLead);
     if (h.ok && slot == kNoSlot) {                             // table full / probe timeout
         h.ok = false;
         h.derr = true;
@@ -1628,74 +1647,52 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     const bool rhead = h.ok && (lane == 0 || pks != ks);
     const bool rtail = h.ok && (lane == 63 || nks != ks);
     const uint64_t RT = __ballot(rtail);
+    // the wave's runs of one key take consecutive indices k (in lane order) from one atomic
+    // of the key's first run head (runs and heads coincide: a run starts at a head)
+    const uint64_t RH = __ballot(rhead);
+    const uint64_t myRuns = same & RH;
+    const bool firstRun = rhead && lead == lane;
+    uint32_t kb = 0;
+    if (firstRun) kb = atomicAdd(&sc.runCnt[slot], (uint32_t)__builtin_popcountll(myRuns));
+    kb = (uint32_t)__shfl((int)kb, (int)lead);
     if (rhead) {
         const uint64_t below = (1ull << lane) - 1ull;
         const uint32_t len = (uint32_t)__builtin_ctzll(RT & ~below) - lane + 1u;   // to this run's last lane
-        const uint32_t k = atomicAdd(&sc.runCnt[slot], 1u);
+        const uint32_t k = kb + (uint32_t)__builtin_popcountll(myRuns & below);
         if (k == 0u) sc.active[atomicAdd(&sc.ctr[1], 1u)] = slot;
         if (k < kRoBucket) {
             sc.bucket[(size_t)slot * kRoBucket + k] = ((unsigned long long)p << 32) | len;
         } else {
             const uint32_t o = atomicAdd(&sc.ctr[0], 1u);
-            st16(reinterpret_cast<uint8_t *>(sc.runs + o), u32x4{slot, p, len, 0u});
+            st16(reinterpret_cast<uint8_t *>(sc.runs + o), u32x4{slot, p, len, k});
         }
     }
     wave_stats(R, live && !foreign, (live && !foreign) ? raw.len : 0u, h.bad, h.derr, wave);
 }
 
-// One workgroup between the key pass and the walk: hands the count of listed keys to the walk
-// and resets the filing counters for the next batch.  Only when some key filed more than
-// kRoBucket runs (ctr[0] > 0 -- heavily reordered or very large events) does it do more: a
-// scan of those slots' run counts gives each its place, its bucket and its overflow runs are
-// copied there, and they are sorted by position (in LDS up to kRoSegLds runs, else a padded
-// bitonic sort in global memory).
-constexpr uint32_t kPlaceThreads = 256, kRoSegLds = 2048;
-__device__ __forceinline__ void bitonic_lds(unsigned long long *v, uint32_t P)
-{
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += kPlaceThreads) {
-                const uint32_t q = i ^ j;
-                if (q > i) {
-                    const unsigned long long x = v[i], y = v[q];
-                    const bool up = (i & k) == 0u;
-                    if (up ? x > y : x < y) v[i] = y, v[q] = x;
-                }
-            }
-            __syncthreads();
-        }
-}
-__device__ __forceinline__ void bitonic_global(unsigned long long *v, uint32_t P)
-{
-    for (uint32_t k = 2; k <= P; k <<= 1)
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t i = threadIdx.x; i < P; i += kPlaceThreads) {
-                const uint32_t q = i ^ j;
-                if (q > i) {
-                    const unsigned long long x = v[i], y = v[q];
-                    const bool up = (i & k) == 0u;
-                    if (up ? x > y : x < y) v[i] = y, v[q] = x;
-                }
-            }
-            __threadfence_block();
-            __syncthreads();
-        }
-}
+// Between the key pass and the walk: hands the count of listed keys to the walk (ctr[1] ->
+// ctr[2]) and resets it for the next batch (ctr[0] is reset by the walk: every workgroup
+// here reads it).  Only when some key filed more than kRoBucket runs (ctr[0] > 0: events
+// interleaved in arrival, or very large ones) does it do more: an exclusive scan of the run
+// counts of those keys gives each its place (runBase), and every overflow run is copied to
+// runBase + its index in the key (k, from the key pass's count) -- no atomics, no order: the
+// key's walk wave sorts them.  Every workgroup computes the scan itself, into LDS (no grid
+// synchronisation), and places a share of the runs; a table above kPlaceLdsSlots slots is
+// handled by workgroup 0 alone through the global runBase.
+constexpr uint32_t kPlaceThreads = 256, kPlaceBlocks = 64, kPlaceLdsSlots = 16384;
 __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, uint32_t T)
 {
+    __shared__ uint32_t base[kPlaceLdsSlots];
     __shared__ uint32_t part[kPlaceThreads];
-    __shared__ unsigned long long seg[kRoSegLds];
-    __shared__ uint32_t big[kPlaceThreads], nBig;
     const uint32_t t = threadIdx.x;
     const uint32_t nOver = sc.ctr[0];
-    if (t == 0) nBig = 0u;
-    __syncthreads();
-    if (t == 0) {
+    if (blockIdx.x == 0 && t == 0) {
         sc.ctr[2] = sc.ctr[1];
         sc.ctr[1] = 0u;
-        sc.ctr[0] = 0u;
     }
     if (nOver == 0u) return;                                          // uniform: the usual case
+    const bool inLds = T <= kPlaceLdsSlots;
+    if (!inLds && blockIdx.x != 0) return;
     const uint32_t per = (T + kPlaceThreads - 1u) / kPlaceThreads;
     const uint32_t s0 = t * per < T ? t * per : T, s1 = s0 + per < T ? s0 + per : T;
     uint32_t sum = 0;
@@ -1714,48 +1711,16 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
     uint32_t b = part[t] - sum;
     for (uint32_t q = s0; q < s1; q++) {
         const uint32_t c = sc.runCnt[q];
-        if (c <= kRoBucket) continue;
-        sc.runBase[q] = b;
-        sc.cursor[q] = b + kRoBucket;
-        for (uint32_t k = 0; k < kRoBucket; k++) sc.placed[b + k] = sc.bucket[(size_t)q * kRoBucket + k];
-        const uint32_t i = atomicAdd(&nBig, 1u);
-        if (i < kPlaceThreads) big[i] = q;
-        b += c;
+        if (inLds) base[q] = b;
+        if (blockIdx.x == 0) sc.runBase[q] = b;
+        b += c > kRoBucket ? c : 0u;
     }
-    __threadfence_block();
-    __syncthreads();
-    for (uint32_t r = t; r < nOver; r += kPlaceThreads) {
-        const RoRun run = sc.runs[r];
-        const uint32_t pos = atomicAdd(&sc.cursor[run.slot], 1u);
-        sc.placed[pos] = ((unsigned long long)run.start << 32) | run.len;
-    }
-    __threadfence_block();
-    __syncthreads();
-    // the LDS list holds up to kPlaceThreads slots; past that every slot is looked at
-    const bool over = nBig > kPlaceThreads;
-    const uint32_t nb = over ? T : nBig;
-    for (uint32_t i = 0; i < nb; i++) {
-        const uint32_t q = over ? i : big[i];
-        const uint32_t c = sc.runCnt[q];
-        if (c <= kRoBucket) continue;                                 // uniform over the workgroup
-        unsigned long long *g = sc.placed + sc.runBase[q];
-        uint32_t P = 1;
-        while (P < c) P <<= 1;
-        if (P <= kRoSegLds) {
-            for (uint32_t k = t; k < P; k += kPlaceThreads) seg[k] = k < c ? g[k] : ~0ull;
-            __syncthreads();
-            bitonic_lds(seg, P);
-            for (uint32_t k = t; k < c; k += kPlaceThreads) g[k] = seg[k];
-            __syncthreads();
-        } else {
-            for (uint32_t k = t; k < P; k += kPlaceThreads) sc.sortTmp[k] = k < c ? g[k] : ~0ull;
-            __threadfence_block();
-            __syncthreads();
-            bitonic_global(sc.sortTmp, P);
-            for (uint32_t k = t; k < c; k += kPlaceThreads) g[k] = sc.sortTmp[k];
-            __threadfence_block();
-            __syncthreads();
-        }
+    __syncthreads();                        // (global runBase: written and read by this workgroup)
+    const uint32_t nThreads = inLds ? gridDim.x * kPlaceThreads : kPlaceThreads;
+    for (uint32_t r = (inLds ? blockIdx.x * kPlaceThreads : 0u) + t; r < nOver; r += nThreads) {
+        const u32x4 run = ld16(reinterpret_cast<const uint8_t *>(sc.runs + r));   // slot, start, len, k
+        const uint32_t rb = inLds ? base[run.x] : sc.runBase[run.x];
+        sc.placed[rb + run.w] = ((unsigned long long)run.y << 32) | run.z;
     }
 }
 
@@ -1772,9 +1737,92 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
 // data errors and add nothing.  One segment per chunk is the usual case; duplicates, late
 // offset-0 fragments and replays after completion add segments.
 constexpr uint32_t kRoAhead = 4;
+constexpr uint32_t kRoSortLds = 2048;       // runs of one key sorted in LDS by its wave (16 KiB)
+
+// Bitonic sort of P = 128 NP keys in LDS by one wave: per stage each lane loads its NP
+// pairs at once (one LDS round trip per stage, not one per pair), then compares and stores.
+template <int NP>
+__device__ __forceinline__ void wave_sort_lds(unsigned long long *v, uint32_t lane)
+{
+    constexpr uint32_t P = 128u * NP;
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            unsigned long long x[NP], y[NP];
+            uint32_t ii[NP];
+#pragma unroll
+            for (uint32_t t = 0; t < (uint32_t)NP; t++) {
+                const uint32_t q = lane + 64u * t;                   // pair q: elements i, i + j
+                ii[t] = ((q & ~(j - 1u)) << 1) | (q & (j - 1u));
+                x[t] = v[ii[t]];
+                y[t] = v[ii[t] + j];
+            }
+#pragma unroll
+            for (uint32_t t = 0; t < (uint32_t)NP; t++) {
+                const bool up = (ii[t] & k) == 0u;
+                if (up ? x[t] > y[t] : x[t] < y[t]) {
+                    v[ii[t]] = y[t];
+                    v[ii[t] + j] = x[t];
+                }
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        }
+}
+
+// Runs of a key of more than kRoBucket runs, in position order, for its walk wave: the
+// bucket (bv, one run per lane) and the placed overflow runs (index >= kRoBucket), padded to
+// a power of two and sorted by start -- up to kRoSortLds runs by a bitonic wave sort in the
+// wave's LDS region, else in its region of sortTmp (at twice the
+// key's place, so regions of different keys never meet) through agent-scope loads and
+// stores, which every lane of the wave sees after the stage's vmcnt(0).  Returns where the
+// sorted runs are.
+__device__ unsigned long long *ro_sort_runs(const RoScratch &sc, uint32_t slot, uint32_t c, unsigned long long bv,
+                                            unsigned long long *lds, uint32_t lane)
+{
+    const uint32_t rb = sc.runBase[slot];
+    const unsigned long long *ov = sc.placed + rb;
+    uint32_t P = 64;
+    while (P < c) P <<= 1;
+    if (P <= kRoSortLds) {
+        for (uint32_t i = lane; i < P; i += 64u) lds[i] = i < kRoBucket ? bv : (i < c ? ov[i] : ~0ull);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        if (P <= 128u) wave_sort_lds<1>(lds, lane);
+        else if (P <= 256u) wave_sort_lds<2>(lds, lane);
+        else if (P <= 512u) wave_sort_lds<4>(lds, lane);
+        else if (P <= 1024u) wave_sort_lds<8>(lds, lane);
+        else wave_sort_lds<16>(lds, lane);
+        return lds;
+    }
+    unsigned long long *g = sc.sortTmp + 2ull * rb;
+    for (uint32_t i = lane; i < P; i += 64u)
+        __hip_atomic_store(g + i, i < kRoBucket ? bv : (i < c ? ov[i] : ~0ull), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    for (uint32_t k = 2; k <= P; k <<= 1)
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = lane; i < P; i += 64u) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const unsigned long long x = __hip_atomic_load(g + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const unsigned long long y = __hip_atomic_load(g + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (((i & k) == 0u) ? x > y : x < y) {
+                        __hip_atomic_store(g + i, y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        __hip_atomic_store(g + l, x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    }
+                }
+            }
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
+    return g;
+}
+
 __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint32_t T, uint64_t now,
                                                          PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
 {
+    __shared__ unsigned long long roSort[kBlock / 64][kRoSortLds];
     const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     // the chain of dependent loads before the walk proper is kept short: the key is read
@@ -1785,7 +1833,9 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     const uint32_t nRuns = sc.runCnt[slot];
     const unsigned long long bv = sc.bucket[(size_t)slot * kRoBucket + lane];
     const bool inBucket = nRuns <= kRoBucket;
-    const unsigned long long *__restrict__ runsOf = inBucket ? nullptr : sc.placed + sc.runBase[slot];
+    if (w == 0 && lane == 0) sc.ctr[0] = 0u;                   // overflow runs: next batch
+    const unsigned long long *runsOf = nullptr;
+    if (!inBucket) runsOf = ro_sort_runs(sc, slot, nRuns, bv, roSort[threadIdx.x >> 6], lane);
     const RoRec *__restrict__ recs = sc.recs;
     ReasSlot *sl = R.slots + slot;
     const uint64_t ev = sl->eventNum;
@@ -2588,7 +2638,7 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     const RoScratch sc = ro_scratch_layout(scratch, n, R.tableSlots);
     hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
                        sc, info);
-    hipLaunchKernelGGL(ro_place_kernel, dim3(1), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots);
+    hipLaunchKernelGGL(ro_place_kernel, dim3(kPlaceBlocks), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
     hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, R.tableSlots, now, info,

@@ -141,28 +141,27 @@ struct RoRec {
 };
 static_assert(sizeof(RoRec) == 16, "one dwordx4 per datagram");
 struct RoRun {
-    uint32_t slot, start, len, pad;
+    uint32_t slot, start, len, k;   // k: the run's index among its key's runs (the key pass's count)
 };
 static_assert(sizeof(RoRun) == 16, "one dwordx4 per run");
 struct RoScratch {
     uint32_t *ctr;                  // [0] overflow runs, [1] keys with runs (both zero between batches),
                                     // [2] keys with runs for the walk
     uint32_t *runCnt;               // [T] runs per slot                        (zero between batches)
-    uint32_t *runBase;              // [T] first placed run of a slot of more than kRoBucket runs
-    uint32_t *cursor;               // [T] placement cursor
+    uint32_t *runBase;              // [T] place of a slot of more than kRoBucket runs (runs k >= kRoBucket at + k)
     uint32_t *active;               // [T] slots with runs in this batch
     unsigned long long *bucket;     // [T][kRoBucket] start << 32 | len, in filing order
     RoRec *recs;                    // [n]
     RoRun *runs;                    // [n] overflow runs
-    unsigned long long *placed;     // [n] runs of the slots of more than kRoBucket runs, in position order
-    unsigned long long *sortTmp;    // [2n] padded sort of a slot's runs (only for slots of > 2048 runs)
+    unsigned long long *placed;     // [n] overflow runs of the slots of more than kRoBucket runs, by k
+    unsigned long long *sortTmp;    // [2n] a slot's padded sort at 2 x runBase (slots of > 2048 runs)
 };
 inline size_t ro_align(size_t x) { return (x + 255) & ~(size_t)255; }
 // the scratch's first bytes that must be zero before its first batch (later batches leave them zero)
 inline size_t ro_zero_bytes(uint32_t T) { return 256 + ro_align(4ull * T); }
 inline size_t ro_scratch_bytes(uint32_t n, uint32_t T)
 {
-    return ro_zero_bytes(T) + 3 * ro_align(4ull * T) + ro_align(8ull * kRoBucket * T) + ro_align(16ull * n) +
+    return ro_zero_bytes(T) + 2 * ro_align(4ull * T) + ro_align(8ull * kRoBucket * T) + ro_align(16ull * n) +
            ro_align(16ull * n) + ro_align(8ull * n) + ro_align(16ull * n);
 }
 inline RoScratch ro_scratch_layout(void *base, uint32_t n, uint32_t T)
@@ -173,9 +172,8 @@ inline RoScratch ro_scratch_layout(void *base, uint32_t n, uint32_t T)
     s.runCnt = reinterpret_cast<uint32_t *>(b + 256);
     b += ro_zero_bytes(T);
     s.runBase = reinterpret_cast<uint32_t *>(b);
-    s.cursor = reinterpret_cast<uint32_t *>(b + ro_align(4ull * T));
-    s.active = reinterpret_cast<uint32_t *>(b + 2 * ro_align(4ull * T));
-    b += 3 * ro_align(4ull * T);
+    s.active = reinterpret_cast<uint32_t *>(b + ro_align(4ull * T));
+    b += 2 * ro_align(4ull * T);
     s.bucket = reinterpret_cast<unsigned long long *>(b);
     b += ro_align(8ull * kRoBucket * T);
     s.recs = reinterpret_cast<RoRec *>(b);

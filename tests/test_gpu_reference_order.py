@@ -225,6 +225,44 @@ def test_large_events_shuffled_with_duplicates(hip, mode):
     assert lost == rlost and loss == rloss
 
 
+@pytest.mark.parametrize("nev,ev_bytes", [(3, 1 << 20), (2, 5 << 20)])
+def test_interleaved_events_many_runs(hip, nev, ev_bytes):
+    """Events interleaved datagram by datagram (concurrent senders): every run of one key is
+    one datagram long, so each key files hundreds to thousands of runs -- its bucket
+    overflows, the runs are placed by their index and sorted by the key's walk wave (in LDS
+    up to 2048 runs: 3 x 1 MiB, 731 runs each; in global memory above: 2 x 5 MiB, 3651 runs
+    each).  A late offset 0 and a duplicate ride along."""
+    rnd = random.Random(nev)
+    mp = O.max_pld_len(1500)
+    stride = (36 + mp + 15) // 16 * 16
+    seqs = []
+    for k in range(nev):
+        ev = np.random.default_rng(700 + k).integers(0, 256, ev_bytes, dtype=np.uint8)
+        pk, ln = O.segment_event(ev, 90 + k, 4321, 1, 2, 2, mp, stride)
+        order = list(range(len(ln)))
+        if k == 0:
+            order = order[1:40] + [0] + order[40:]            # late offset 0: the first 39 are orphaned
+        if k == 1:
+            order.insert(500, order[77])                      # a duplicate before the end
+        seqs.append([(pk[i], int(ln[i])) for i in order])
+    out = []
+    while any(seqs):                                          # round robin over the events
+        for s_ in seqs:
+            if s_:
+                out.append(s_.pop(0))
+    pk = np.stack([p for p, _ in out])
+    ln = np.array([L for _, L in out], np.uint32)
+    ref, rst, rlost, rloss, rinp = _oracle(pk, ln)
+    n = len(ln)
+    for mode in ("fused", "pipelined"):
+        got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, n // 2, n], mode)
+        assert st == rst, (mode, st, rst)
+        assert sorted(got) == sorted(ref), mode
+        for k in ref:
+            assert sorted(got[k]) == sorted(ref[k]), (k, mode)
+        assert lost == rlost and loss == rloss and inp == rinp, mode
+
+
 def test_reference_order_in_a_replayed_graph(hip):
     """Reference-order launches captured in a HIP graph and replayed: the key pass's run
     filing holds no memset node (its counters are reset by the kernels that use them, a

@@ -1663,24 +1663,31 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         if (k < kRoBucket) {
             sc.bucket[(size_t)slot * kRoBucket + k] = ((unsigned long long)p << 32) | len;
         } else {
-            const uint32_t o = atomicAdd(&sc.ctr[0], 1u);
-            st16(reinterpret_cast<uint8_t *>(sc.runs + o), u32x4{slot, p, len, k});
+            st16(reinterpret_cast<uint8_t *>(sc.runs + p), u32x4{slot, p, len, k});   // at its head's position
         }
+    }
+    // which lanes of this wave hold an overflow run (every wave writes its word; a flag tells
+    // the place pass to look -- a plain store, not a counter all waves would contend on)
+    const uint64_t OV = __ballot(rhead && kb + (uint32_t)__builtin_popcountll(myRuns & ((1ull << lane) - 1ull)) >= kRoBucket);
+    if (lane == 0) {
+        sc.ovMask[wave] = OV;
+        if (OV) sc.ctr[0] = 1u;
     }
     wave_stats(R, live && !foreign, (live && !foreign) ? raw.len : 0u, h.bad, h.derr, wave);
 }
 
 // Between the key pass and the walk: hands the count of listed keys to the walk (ctr[1] ->
 // ctr[2]) and resets it for the next batch (ctr[0] is reset by the walk: every workgroup
-// here reads it).  Only when some key filed more than kRoBucket runs (ctr[0] > 0: events
+// here reads it).  Only when some key filed more than kRoBucket runs (ctr[0] set: events
 // interleaved in arrival, or very large ones) does it do more: an exclusive scan of the run
-// counts of those keys gives each its place (runBase), and every overflow run is copied to
-// runBase + its index in the key (k, from the key pass's count) -- no atomics, no order: the
-// key's walk wave sorts them.  Every workgroup computes the scan itself, into LDS (no grid
+// counts of those keys gives each its place (runBase), and every overflow run (found by the
+// key-pass waves' overflow masks, stored at its head's position) is copied to runBase + its
+// index in the key (k, from the key pass's count) -- no atomics, no order: the key's walk
+// wave orders them.  Every workgroup computes the scan itself, into LDS (no grid
 // synchronisation), and places a share of the runs; a table above kPlaceLdsSlots slots is
 // handled by workgroup 0 alone through the global runBase.
 constexpr uint32_t kPlaceThreads = 256, kPlaceBlocks = 64, kPlaceLdsSlots = 16384;
-__global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, uint32_t T)
+__global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, uint32_t T, uint32_t n)
 {
     __shared__ uint32_t base[kPlaceLdsSlots];
     __shared__ uint32_t part[kPlaceThreads];
@@ -1716,11 +1723,15 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
         b += c > kRoBucket ? c : 0u;
     }
     __syncthreads();                        // (global runBase: written and read by this workgroup)
+    // one thread per datagram position: an overflow run sits at its head's position, marked
+    // in its key-pass wave's mask
     const uint32_t nThreads = inLds ? gridDim.x * kPlaceThreads : kPlaceThreads;
-    for (uint32_t r = (inLds ? blockIdx.x * kPlaceThreads : 0u) + t; r < nOver; r += nThreads) {
-        const u32x4 run = ld16(reinterpret_cast<const uint8_t *>(sc.runs + r));   // slot, start, len, k
-        const uint32_t rb = inLds ? base[run.x] : sc.runBase[run.x];
-        sc.placed[rb + run.w] = ((unsigned long long)run.y << 32) | run.z;
+    for (uint32_t p = (inLds ? blockIdx.x * kPlaceThreads : 0u) + t; p < n; p += nThreads) {
+        if ((sc.ovMask[p >> 6] >> (p & 63u)) & 1ull) {
+            const u32x4 run = ld16(reinterpret_cast<const uint8_t *>(sc.runs + p));   // slot, start, len, k
+            const uint32_t rb = inLds ? base[run.x] : sc.runBase[run.x];
+            sc.placed[rb + run.w] = ((unsigned long long)run.y << 32) | run.z;
+        }
     }
 }
 
@@ -1819,6 +1830,80 @@ __device__ unsigned long long *ro_sort_runs(const RoScratch &sc, uint32_t slot, 
     return g;
 }
 
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = min(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
+{
+#pragma unroll
+    for (int o = 32; o; o >>= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
+    return v;
+}
+
+// The positions of a key of more than kRoBucket runs, in arrival order, into the wave's LDS
+// region, without sorting its runs: every run sets its positions' bits in a bitmap over the
+// key's span (LDS atomic ORs), and the set bits read in order are the positions.  Returns
+// how many (0 when bitmap and list do not fit the region: then the runs are sorted).
+__device__ uint32_t ro_positions(const RoScratch &sc, uint32_t slot, uint32_t c, unsigned long long bv,
+                                 unsigned long long *lds, uint32_t lane)
+{
+    const unsigned long long *ov = sc.placed + sc.runBase[slot];
+    uint32_t mn = 0xFFFFFFFFu, mx = 0, tl = 0;
+    for (uint32_t i = lane; i < c; i += 64u) {
+        const unsigned long long r = i < kRoBucket ? bv : ov[i];
+        const uint32_t st = (uint32_t)(r >> 32), ln = (uint32_t)r;
+        mn = min(mn, st);
+        mx = max(mx, st + ln);
+        tl += ln;
+    }
+    mn = wave_min_u32(mn);
+    mx = wave_max_u32(mx);
+    tl = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl), 63);
+    const uint32_t words = (mx - mn + 63u) / 64u;
+    if ((size_t)words * 8u + (size_t)tl * 4u > (size_t)kRoSortLds * 8u) return 0u;   // wave-uniform
+    for (uint32_t i = lane; i < words; i += 64u) lds[i] = 0ull;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (uint32_t i = lane; i < c; i += 64u) {
+        const unsigned long long r = i < kRoBucket ? bv : ov[i];
+        const uint32_t b = (uint32_t)(r >> 32) - mn, ln = (uint32_t)r;   // 1..64 positions
+        const unsigned long long m = ln >= 64u ? ~0ull : ((1ull << ln) - 1ull);
+        const uint32_t o = b & 63u;
+        atomicOr(&lds[b >> 6], m << o);
+        if (o + ln > 64u) atomicOr(&lds[(b >> 6) + 1u], m >> (64u - o));
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // each lane reads a contiguous block of words; a wave scan of their counts places them
+    const uint32_t wpl = (words + 63u) / 64u, w0 = lane * wpl, w1 = min(w0 + wpl, words);
+    uint32_t cnt = 0;
+    for (uint32_t x = w0; x < w1; x++) cnt += (uint32_t)__builtin_popcountll(lds[x]);
+    uint32_t at = wave_incl_scan(cnt) - cnt;
+    uint32_t *pos = reinterpret_cast<uint32_t *>(lds + words);
+    for (uint32_t x = w0; x < w1; x++)
+        for (unsigned long long m = lds[x]; m; m &= m - 1ull) pos[at++] = mn + x * 64u + (uint32_t)__builtin_ctzll(m);
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // the list starts at lds + words: move it to the front (the walk reads it from there)
+    uint32_t *dst = reinterpret_cast<uint32_t *>(lds);
+    for (uint32_t i = lane; i < tl; i += 64u) {
+        const uint32_t v = pos[i];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        dst[i] = v;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    return tl;
+}
+
 __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint32_t T, uint64_t now,
                                                          PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
 {
@@ -1834,8 +1919,13 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     const unsigned long long bv = sc.bucket[(size_t)slot * kRoBucket + lane];
     const bool inBucket = nRuns <= kRoBucket;
     if (w == 0 && lane == 0) sc.ctr[0] = 0u;                   // overflow runs: next batch
+    unsigned long long *lds = roSort[threadIdx.x >> 6];
     const unsigned long long *runsOf = nullptr;
-    if (!inBucket) runsOf = ro_sort_runs(sc, slot, nRuns, bv, roSort[threadIdx.x >> 6], lane);
+    uint32_t nPos = 0;                                         // > 0: the key's positions are in lds
+    if (!inBucket) {
+        nPos = ro_positions(sc, slot, nRuns, bv, lds, lane);
+        if (nPos == 0u) runsOf = ro_sort_runs(sc, slot, nRuns, bv, lds, lane);
+    }
     const RoRec *__restrict__ recs = sc.recs;
     ReasSlot *sl = R.slots + slot;
     const uint64_t ev = sl->eventNum;
@@ -1848,40 +1938,7 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     uint64_t created = sl->created;
     long long live = 0;                                        // net change of items in progress
     uint32_t derr = 0;
-    for (uint32_t r0 = 0; r0 < nRuns; r0 += 64u) {
-    // this batch of the key's runs, in position order: start << 32 | length per lane
-    const uint32_t m = (nRuns - r0 < 64u) ? nRuns - r0 : 64u;
-    unsigned long long rv = (lane < m) ? (inBucket ? bv : runsOf[r0 + lane]) : ~0ull;
-    if (inBucket) {
-        // order the bucket by start (the starts are distinct): each run's rank is the number
-        // of runs that start before it (m scalar reads), then one push per word to lane rank
-        const uint32_t mys = (uint32_t)(rv >> 32);
-        uint32_t rank = 0;
-        for (uint32_t r = 0; r < m; r++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mys, (int)r) < mys ? 1u : 0u;
-        if (lane >= m) rank = lane;
-        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)(uint32_t)rv);
-        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)mys);
-        rv = ((unsigned long long)hi << 32) | lo;
-    }
-    const uint32_t rlen = (uint32_t)rv & 0xFFFFFFFFu, rstart = (uint32_t)(rv >> 32);
-    const uint32_t rl = lane < m ? rlen : 0u;
-    const uint32_t rin = wave_incl_scan(rl), rex = rin - rl;
-    const uint32_t tot = (uint32_t)__builtin_amdgcn_readlane((int)rin, 63);
-    // position of datagram base + lane of this batch of runs: in the last run whose prefix
-    // is <= it.  The runs that meet the chunk [base, base + 64) are r0..r1 (usually two): a
-    // uniform loop over them with scalar reads, no per-lane search
-    auto pos_of = [&](uint32_t base) -> uint32_t {
-        const uint32_t g = base + lane;
-        const uint64_t b0 = __ballot(lane < m && rex <= base), b1 = __ballot(lane < m && rex < base + 64u);
-        const int r0 = b0 ? 63 - __builtin_clzll(b0) : 0, r1 = b1 ? 63 - __builtin_clzll(b1) : 0;
-        uint32_t qb = 0;
-        for (int r = r0; r <= r1; r++) {
-            const uint32_t sr = (uint32_t)__builtin_amdgcn_readlane((int)rex, r);
-            const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)rstart, r);
-            if (g >= sr) qb = st - sr;
-        }
-        return qb + g;
-    };
+    uint32_t tot = 0;                                          // datagrams of the current walk
     // one chunk of 64 datagrams of the key, in arrival order (q: position, rc: record)
     auto walk_chunk = [&](uint32_t base, uint32_t q, const RoRec &rc) {
         const bool valid = base + lane < tot;
@@ -1950,11 +2007,12 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     // the chunk is walked.  (Round 5: staging a key's records in LDS by LDS-DMA, 16 chunks per
     // wait, measured 16.6 against this ring's 15.5 us per launch: the chunks' own work, ~0.8
     // us each at one wave per CU, not their loads, bounds the walk)
+    auto walk_ring = [&](auto q_of) {
     uint32_t qr[kRoAhead];
     RoRec rr[kRoAhead];
 #pragma unroll
     for (uint32_t i = 0; i < kRoAhead; i++) {
-        qr[i] = pos_of(i * 64u);
+        qr[i] = q_of(i * 64u);
         rr[i] = RoRec{0u, 0u, 0u, 0u};
         if (i * 64u + lane < tot) rr[i] = recs[qr[i]];
     }
@@ -1966,11 +2024,54 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
                 walk_chunk(base, qr[i], rr[i]);
                 const uint32_t nxt = base + kRoAhead * 64u;
                 if (nxt < tot) {
-                    qr[i] = pos_of(nxt);
+                    qr[i] = q_of(nxt);
                     if (nxt + lane < tot) rr[i] = recs[qr[i]];
                 }
             }
         }
+    }
+    };
+    if (nPos) {
+        // the key's positions in arrival order, from its position bitmap
+        const uint32_t *pos = reinterpret_cast<const uint32_t *>(lds);
+        tot = nPos;
+        walk_ring([&](uint32_t base) -> uint32_t { return base + lane < tot ? pos[base + lane] : 0u; });
+    } else {
+    for (uint32_t r0 = 0; r0 < nRuns; r0 += 64u) {
+    // this batch of the key's runs, in position order: start << 32 | length per lane
+    const uint32_t m = (nRuns - r0 < 64u) ? nRuns - r0 : 64u;
+    unsigned long long rv = (lane < m) ? (inBucket ? bv : runsOf[r0 + lane]) : ~0ull;
+    if (inBucket) {
+        // order the bucket by start (the starts are distinct): each run's rank is the number
+        // of runs that start before it (m scalar reads), then one push per word to lane rank
+        const uint32_t mys = (uint32_t)(rv >> 32);
+        uint32_t rank = 0;
+        for (uint32_t r = 0; r < m; r++) rank += (uint32_t)__builtin_amdgcn_readlane((int)mys, (int)r) < mys ? 1u : 0u;
+        if (lane >= m) rank = lane;
+        const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)(uint32_t)rv);
+        const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_permute((int)(rank * 4u), (int)mys);
+        rv = ((unsigned long long)hi << 32) | lo;
+    }
+    const uint32_t rlen = (uint32_t)rv & 0xFFFFFFFFu, rstart = (uint32_t)(rv >> 32);
+    const uint32_t rl = lane < m ? rlen : 0u;
+    const uint32_t rin = wave_incl_scan(rl), rex = rin - rl;
+    tot = (uint32_t)__builtin_amdgcn_readlane((int)rin, 63);
+    // position of datagram base + lane of this batch of runs: in the last run whose prefix
+    // is <= it.  The runs that meet the chunk [base, base + 64) are r0..r1 (usually two): a
+    // uniform loop over them with scalar reads, no per-lane search
+    auto pos_of = [&](uint32_t base) -> uint32_t {
+        const uint32_t g = base + lane;
+        const uint64_t b0 = __ballot(lane < m && rex <= base), b1 = __ballot(lane < m && rex < base + 64u);
+        const int r0 = b0 ? 63 - __builtin_clzll(b0) : 0, r1 = b1 ? 63 - __builtin_clzll(b1) : 0;
+        uint32_t qb = 0;
+        for (int r = r0; r <= r1; r++) {
+            const uint32_t sr = (uint32_t)__builtin_amdgcn_readlane((int)rex, r);
+            const uint32_t st = (uint32_t)__builtin_amdgcn_readlane((int)rstart, r);
+            if (g >= sr) qb = st - sr;
+        }
+        return qb + g;
+    };
+    walk_ring(pos_of);
     }
     }
     if (lane == 0) {
@@ -2638,7 +2739,7 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     const RoScratch sc = ro_scratch_layout(scratch, n, R.tableSlots);
     hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
                        sc, info);
-    hipLaunchKernelGGL(ro_place_kernel, dim3(kPlaceBlocks), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots);
+    hipLaunchKernelGGL(ro_place_kernel, dim3(kPlaceBlocks), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots, n);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
     hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, R.tableSlots, now, info,

@@ -145,14 +145,15 @@ struct RoRun {
 };
 static_assert(sizeof(RoRun) == 16, "one dwordx4 per run");
 struct RoScratch {
-    uint32_t *ctr;                  // [0] overflow runs, [1] keys with runs (both zero between batches),
+    uint32_t *ctr;                  // [0] overflow flag, [1] keys with runs (both zero between batches),
                                     // [2] keys with runs for the walk
     uint32_t *runCnt;               // [T] runs per slot                        (zero between batches)
     uint32_t *runBase;              // [T] place of a slot of more than kRoBucket runs (runs k >= kRoBucket at + k)
     uint32_t *active;               // [T] slots with runs in this batch
     unsigned long long *bucket;     // [T][kRoBucket] start << 32 | len, in filing order
     RoRec *recs;                    // [n]
-    RoRun *runs;                    // [n] overflow runs
+    RoRun *runs;                    // [n] overflow runs, at their head datagram's position
+    unsigned long long *ovMask;     // [n / 64] per key-pass wave: lanes that head an overflow run
     unsigned long long *placed;     // [n] overflow runs of the slots of more than kRoBucket runs, by k
     unsigned long long *sortTmp;    // [2n] a slot's padded sort at 2 x runBase (slots of > 2048 runs)
 };
@@ -162,7 +163,7 @@ inline size_t ro_zero_bytes(uint32_t T) { return 256 + ro_align(4ull * T); }
 inline size_t ro_scratch_bytes(uint32_t n, uint32_t T)
 {
     return ro_zero_bytes(T) + 2 * ro_align(4ull * T) + ro_align(8ull * kRoBucket * T) + ro_align(16ull * n) +
-           ro_align(16ull * n) + ro_align(8ull * n) + ro_align(16ull * n);
+           ro_align(16ull * n) + ro_align(8ull * n) + ro_align(16ull * n) + ro_align(8ull * ((n + 63) / 64));
 }
 inline RoScratch ro_scratch_layout(void *base, uint32_t n, uint32_t T)
 {
@@ -183,6 +184,8 @@ inline RoScratch ro_scratch_layout(void *base, uint32_t n, uint32_t T)
     s.placed = reinterpret_cast<unsigned long long *>(b);
     b += ro_align(8ull * n);
     s.sortTmp = reinterpret_cast<unsigned long long *>(b);
+    b += ro_align(16ull * n);
+    s.ovMask = reinterpret_cast<unsigned long long *>(b);
     return s;
 }
 hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t stride, const uint32_t *lens,

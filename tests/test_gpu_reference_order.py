@@ -121,14 +121,14 @@ def _draw(seed):
     return pk, ln, stride, rnd
 
 
-def _gpu(ctx, pk, ln, stride, cuts, mode, now0=100):
+def _gpu(ctx, pk, ln, stride, cuts, mode, now0=100, arena=64 << 20, slots=256):
     import torch
     from e2sar_amd import sar
     n = len(ln)
     dpk = torch.from_numpy(np.ascontiguousarray(pk).reshape(-1)).to(ctx.torch_device)
     dln = torch.from_numpy(ln.view(np.int32).copy()).to(ctx.torch_device)
-    R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=256, queue_capacity=4096, lost_capacity=4096,
-                              arena_bytes=64 << 20, flags=_flag())
+    R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=slots, queue_capacity=4096, lost_capacity=4096,
+                              arena_bytes=arena, flags=_flag())
     spans = [(a, b) for a, b in zip(cuts[:-1], cuts[1:]) if b > a]
     works = [R.alloc_work(n) for _ in range(2)]
     if mode == "pipelined":
@@ -261,6 +261,32 @@ def test_interleaved_events_many_runs(hip, nev, ev_bytes):
         for k in ref:
             assert sorted(got[k]) == sorted(ref[k]), (k, mode)
         assert lost == rlost and loss == rloss and inp == rinp, mode
+
+
+@pytest.mark.parametrize("nev,ev_bytes", [(160, 1 << 20), (28, 3 << 20)])
+def test_interleaved_wide_span_sorts_runs(hip, nev, ev_bytes):
+    """Many events interleaved datagram by datagram: a key's span is too wide for the walk
+    wave's position bitmap, so its runs are sorted -- 160 x 1 MiB (731 runs per key) by the
+    bitonic wave sort in LDS, 28 x 3 MiB (2192 runs per key) in global memory."""
+    mp = O.max_pld_len(1500)
+    stride = (36 + mp + 15) // 16 * 16
+    pks, lns = [], []
+    for k in range(nev):
+        ev = np.random.default_rng(1100 + k).integers(0, 256, ev_bytes, dtype=np.uint8)
+        pk, ln = O.segment_event(ev, 300 + k, 4321, 1, 2, 2, mp, stride)
+        pks.append(pk)
+        lns.append(ln)
+    pk = np.stack(pks).transpose(1, 0, 2).reshape(-1, pks[0].shape[1])   # round robin over the events
+    ln = np.stack(lns).T.reshape(-1)
+    ref, rst, rlost, rloss, rinp = _oracle(pk, ln)
+    n = len(ln)
+    # one batch: the whole span in one walk (a cut would leave each batch's span narrow enough)
+    got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, n], "fused", arena=nev * ev_bytes + (8 << 20), slots=1024)
+    assert st == rst, (st, rst)
+    assert sorted(got) == sorted(ref) and len(ref) == nev
+    for k in ref:
+        assert sorted(got[k]) == sorted(ref[k]), k
+    assert lost == rlost and loss == rloss and inp == rinp
 
 
 def test_reference_order_in_a_replayed_graph(hip):

@@ -185,8 +185,9 @@ typedef struct e2sar_hip_reas_config {
  * order in the batch.  Without the flag the device path is order-insensitive: every
  * fragment joins its event and completion is tested per run of a launch (identical results
  * whenever offset 0 arrives first and there are no duplicates).  The mode
- * adds a key pass and a per-key walk per batch and device scratch (about 72 bytes per
- * datagram of the largest batch plus 524 bytes per table slot) that grows on demand (per stream; it cannot
+ * adds a key pass and a per-key walk per batch and device scratch (about 56 bytes per
+ * datagram of the largest batch, 48 more in reassemble_batch for its work records, and 524
+ * bytes per table slot) that grows on demand (per stream; it cannot
  * grow inside a graph capture -- such a launch fails with LOGIC -- so capture only after a
  * first batch of the largest size has run on the capturing stream). */
 #define E2SAR_HIP_REAS_REFERENCE_ORDER 2u

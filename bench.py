@@ -29,6 +29,7 @@ import os
 import socket
 import subprocess
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -352,7 +353,24 @@ def main():
         over = SUB_LEGS[name]
         a = argparse.Namespace(**{**vars(args), **over, "cold_steps": 0, "cpu_seconds": 0.0})
         t0 = time.perf_counter()
-        sl = run_workload(a, env, headline=False)
+        # At N > 1 a sub-leg runs collectives (the spread leg's RCCL all-to-alls): should one
+        # fail or stall, the headline measured above is still reported -- rank 0 prints its
+        # line with the sub-leg's error and every rank exits (os._exit: a rank stuck in a
+        # collective cannot return) once the deadline passes
+        guard = None
+        if world > 1:
+            deadline = float(os.environ.get("E2SAR_SUBLEG_DEADLINE_S", "420"))
+            guard = threading.Timer(deadline, _abandon_sub_leg, args=(line, name, rank, f"no result in {deadline:.0f} s"))
+            guard.daemon = True
+            guard.start()
+        try:
+            sl = run_workload(a, env, headline=False)
+        except Exception as e:                  # noqa: BLE001 -- reported, not swallowed
+            if world == 1:
+                raise
+            _abandon_sub_leg(line, name, rank, f"{type(e).__name__}: {e}"[:400])
+        if guard is not None:
+            guard.cancel()
         torch.cuda.empty_cache()
         if rank == 0:
             line[name] = {
@@ -370,6 +388,17 @@ def main():
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def _abandon_sub_leg(line, name: str, rank: int, why: str):
+    """A sub-leg at N > 1 failed or stalled: rank 0 prints the run's line (the headline and
+    the sub-legs done so far) with this one's error; every rank ends here."""
+    if rank == 0:
+        line[name] = {"error": why}
+        print(json.dumps(line), flush=True)
+    sys.stderr.write(f"bench: rank {rank}: sub-leg {name} abandoned ({why})\n")
+    sys.stderr.flush()
+    os._exit(0)
 
 
 def sub_legs(args, world: int):

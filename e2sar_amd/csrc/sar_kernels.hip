@@ -1579,18 +1579,27 @@ __global__ __launch_bounds__(TB) void reas_scatter_classify_kernel(
 // key of a datagram that does not take part (bad header, bounds, table full): no real slot,
 // so it joins no run
 constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
+constexpr uint32_t kWgKeys = 2u * kBlock;       // the key pass's per-workgroup key table
 
 __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
                                                         const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
                                                         RoScratch sc, PktInfo *__restrict__ info)
 {
+    // the workgroup's distinct keys (at most kBlock): one global lookup and one run-count
+    // atomic per key per workgroup, not per wave
+    __shared__ unsigned long long wgEv[kWgKeys];
+    __shared__ uint32_t wgD[kWgKeys], wgTag[kWgKeys], wgCnt[kWgKeys], wgSlot[kWgKeys], wgBase[kWgKeys];
     const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t p0 = wave * 64u;
-    if (p0 >= n) return;                                       // wave-uniform
-    const uint32_t gn = (n - p0 < 64u) ? n - p0 : 64u;
+    const bool waveLive = p0 < n;                              // (a wave past n still meets the barriers)
+    const uint32_t gn = !waveLive ? 0u : (n - p0 < 64u) ? n - p0 : 64u;
     const bool live = lane < gn;
-    const uint32_t p = p0 + (live ? lane : 0u);
+    const uint32_t p = waveLive ? p0 + (live ? lane : 0u) : 0u;
+    for (uint32_t i = threadIdx.x; i < kWgKeys; i += kBlock) {
+        wgTag[i] = 0u;
+        wgCnt[i] = 0u;
+    }
     const RawHdr raw = load_hdr(R, pkts, stride, lens, p);
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
     ParsedHdr h = parse_hdr(raw, hl, stride, live);
@@ -1624,13 +1633,49 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         pend &= ~m;
     }
     const bool leader = head && lead == lane;
-    const LookupResult lr = find_or_create<true>(R, leader, h.ev, h.d, h.blen, now);
+    // each wave's leaders claim or find their key's entry in the workgroup's table
+    uint32_t e = slot_hash(h.ev, h.d, kWgKeys - 1u);
+    bool pending = leader, check = false;
+    __syncthreads();                                           // table cleared
+    while (__syncthreads_or(pending)) {
+        if (pending) {
+            if (atomicCAS(&wgTag[e], 0u, 1u) == 0u) {
+                wgEv[e] = h.ev;
+                wgD[e] = h.d;
+                pending = false;
+            } else {
+                check = true;
+            }
+        }
+        __syncthreads();                                       // claimed keys are written
+        if (check) {
+            check = false;
+            if (wgEv[e] == h.ev && wgD[e] == h.d) pending = false;
+            else e = (e + 1u) & (kWgKeys - 1u);
+        }
+    }
+    // this wave's runs of the key (its heads): their offset among the workgroup's runs of it
+    uint32_t o = 0;
+    if (leader) o = atomicAdd(&wgCnt[e], (uint32_t)__builtin_popcountll(same));
+    __syncthreads();
+    for (uint32_t b = 0; b < kWgKeys; b += kBlock) {           // one lookup + one atomic per key
+        const uint32_t i = b + threadIdx.x;
+        const bool want = wgTag[i] != 0u;
+        const LookupResult lr = find_or_create<true>(R, want, wgEv[i], wgD[i], 0u, now);
+        if (want) {
+            wgSlot[i] = lr.slot;
+            wgBase[i] = lr.slot != kNoSlot ? atomicAdd(&sc.runCnt[lr.slot], wgCnt[i]) : 0u;
+        }
+    }
+    __syncthreads();
+    const uint32_t lslot = leader ? wgSlot[e] : kNoSlot;
+    const uint32_t lkb = leader ? wgBase[e] + o : 0u;
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const uint64_t hm = H & le;
     const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
     const uint32_t keyLead = __shfl(lead, myhead);
-    const uint32_t slot = __shfl(lr.slot, (int)keyLead);
+    const uint32_t slot = __shfl(lslot, (int)keyLead);
     if (h.ok && slot == kNoSlot) {                             // table full / probe timeout
         h.ok = false;
         h.derr = true;
@@ -1647,14 +1692,11 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     const bool rhead = h.ok && (lane == 0 || pks != ks);
     const bool rtail = h.ok && (lane == 63 || nks != ks);
     const uint64_t RT = __ballot(rtail);
-    // the wave's runs of one key take consecutive indices k (in lane order) from one atomic
-    // of the key's first run head (runs and heads coincide: a run starts at a head)
+    // the wave's runs of one key take consecutive indices k (in lane order) from the
+    // workgroup's block of the key (runs and heads coincide: a run starts at a head)
     const uint64_t RH = __ballot(rhead);
     const uint64_t myRuns = same & RH;
-    const bool firstRun = rhead && lead == lane;
-    uint32_t kb = 0;
-    if (firstRun) kb = atomicAdd(&sc.runCnt[slot], (uint32_t)__builtin_popcountll(myRuns));
-    kb = (uint32_t)__shfl((int)kb, (int)lead);
+    const uint32_t kb = (uint32_t)__shfl((int)lkb, (int)lead);
     if (rhead) {
         const uint64_t below = (1ull << lane) - 1ull;
         const uint32_t len = (uint32_t)__builtin_ctzll(RT & ~below) - lane + 1u;   // to this run's last lane
@@ -1669,7 +1711,7 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     // which lanes of this wave hold an overflow run (every wave writes its word; a flag tells
     // the place pass to look -- a plain store, not a counter all waves would contend on)
     const uint64_t OV = __ballot(rhead && kb + (uint32_t)__builtin_popcountll(myRuns & ((1ull << lane) - 1ull)) >= kRoBucket);
-    if (lane == 0) {
+    if (lane == 0 && waveLive) {
         sc.ovMask[wave] = OV;
         if (OV) sc.ctr[0] = 1u;
     }

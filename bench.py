@@ -258,10 +258,12 @@ def graph_steps(args) -> int:
         return args.graph_steps
     return next(d for d in (4, 2, 1) if args.steps % d == 0)
 
-def _pmc_traffic(args, dom):
+def _pmc_traffic(args, dom, batch_events=None):
     """HBM traffic per launch of kernel `dom` from the committed rocprofv3 PMC summaries
     (tools/pmc_summary.py; FETCH_SIZE x2 + WRITE_SIZE, gfx950 rules) whose workload is this
-    one: profiles/pmc_latest.json and profiles/pmc_*.json."""
+    one: profiles/pmc_latest.json and profiles/pmc_*.json.  batch_events: the events per
+    launch of the leg asking (the cold leg launches its own batch, not --batch-events)."""
+    be = args.batch_events if batch_events is None else batch_events
     import glob
     for path in [os.path.join(ROOT, "profiles", "pmc_latest.json")] + sorted(
             glob.glob(os.path.join(ROOT, "profiles", "pmc_*.json"))):
@@ -272,7 +274,7 @@ def _pmc_traffic(args, dom):
             continue
         w = pmc.get("workload") or {}
         if (w.get("mtu") == args.mtu and w.get("event_bytes") == args.event_bytes
-                and w.get("batch_events") == args.batch_events and w.get("lb_version", 2) == args.lb_version):
+                and w.get("batch_events") == be and w.get("lb_version", 2) == args.lb_version):
             ks = pmc.get("kernels") or {}
             # reassemble_batch's split form (batches above 320 MiB of slots) is two launches
             parts = ("reas_classify_kernel", "reas_scatter_kernel") if dom == "reassemble_batch_split" else (dom,)
@@ -385,20 +387,37 @@ def main():
     if rank == 0 and world == 1 and args.cpu_seconds > 0:
         line["cpu_baseline"] = cpu_baseline(args, args.cpu_seconds)
     if rank == 0:
-        print(json.dumps(line), flush=True)
+        _print_line(line)
     if world > 1:
         dist.destroy_process_group()
 
 
+_LINE_LOCK = threading.Lock()
+_LINE_PRINTED = [False]
+
+
+def _print_line(line):
+    """Rank 0's one JSON line, printed once: the deadline timer's thread and the main
+    thread may both reach here."""
+    with _LINE_LOCK:
+        if _LINE_PRINTED[0]:
+            return
+        _LINE_PRINTED[0] = True
+        print(json.dumps(line), flush=True)
+
+
 def _abandon_sub_leg(line, name: str, rank: int, why: str):
     """A sub-leg at N > 1 failed or stalled: rank 0 prints the run's line (the headline and
-    the sub-legs done so far) with this one's error; every rank ends here."""
+    the sub-legs done so far) with this one's error; every rank ends here with status 3, so
+    torchrun and CI see the failure (the headline in the line stays readable)."""
     if rank == 0:
-        line[name] = {"error": why}
-        print(json.dumps(line), flush=True)
+        with _LINE_LOCK:
+            if not _LINE_PRINTED[0]:
+                line[name] = {"error": why}
+        _print_line(line)
     sys.stderr.write(f"bench: rank {rank}: sub-leg {name} abandoned ({why})\n")
     sys.stderr.flush()
-    os._exit(0)
+    os._exit(3)
 
 
 def sub_legs(args, world: int):
@@ -931,7 +950,7 @@ def run_workload(args, env, headline: bool):
                          "all_launch_ms": {k: round(sum(v) / len(v), 5) for k, v in cper.items()}},
             "flags": "E2SAR_HIP_REAS_COLD_DATAGRAMS",
         }
-        ctr, csrc = _pmc_traffic(args, ckern)
+        ctr, csrc = _pmc_traffic(args, ckern, batch_events=cb)
         cold["roofline"]["traffic"] = ctr
         if ctr is not None:
             cold["roofline"]["traffic_unit"] = "bytes per launch (rocprofv3 PMC, committed)"

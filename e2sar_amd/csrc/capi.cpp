@@ -81,6 +81,9 @@ struct e2sar_hip_reas {
     struct Scratch {
         void *roScratch = nullptr;
         size_t roScratchBytes = 0;
+        // a reference-order launch sequence failed part way: the key pass may have left run
+        // counts that only the place / walk kernels reset, so the next batch re-zeroes them
+        bool roDirty = false;
         void *roWork = nullptr;
         size_t roWorkBytes = 0;
         void *tiles = nullptr;
@@ -606,7 +609,19 @@ static int ro_prepare(e2sar_hip_reas *r, hipStream_t s, uint32_t n)
     bool grew = false;
     if (int rc = grow(r, s, sc.roScratch, sc.roScratchBytes, ro_scratch_bytes(n, r->dev.tableSlots), &grew)) return rc;
     if (grew) HIP_TRY(hipMemsetAsync(sc.roScratch, 0, ro_zero_bytes(r->dev.tableSlots), s));
+    else if (sc.roDirty) HIP_TRY(launch_fill_bytes(sc.roScratch, 0, ro_zero_bytes(r->dev.tableSlots), s));  // capture-safe
+    sc.roDirty = false;
     return E2SAR_HIP_OK;
+}
+
+// launch_ro_classify, remembering a failure part way through its launches (ro_prepare)
+static hipError_t ro_classify(e2sar_hip_reas *r, hipStream_t s, const uint8_t *pk, uint32_t stride, const uint32_t *lens,
+                              uint32_t n, uint64_t now, void *work)
+{
+    auto &sc = r->scratch[s];
+    const hipError_t e = launch_ro_classify(r->dev, pk, stride, lens, n, now, work, sc.roScratch, sc.roScratchBytes, s);
+    if (e != hipSuccess) sc.roDirty = true;
+    return e;
 }
 
 extern "C" {
@@ -629,8 +644,7 @@ int e2sar_hip_reassemble_batch(e2sar_hip_reas *r, const uint8_t *d_packets, uint
         // classify in arrival order into the internal work buffer, then the scatter kernel
         if (int rc = ro_prepare(r, s, nPackets)) return rc;
         if (int rc = grow(r, s, sc.roWork, sc.roWorkBytes, work_bytes(nPackets))) return rc;
-        hipError_t e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork,
-                                          sc.roScratch, sc.roScratchBytes, s);
+        hipError_t e = ro_classify(r, s, d_packets, stride, d_lens, nPackets, now_ms, sc.roWork);
         if (e == hipSuccess)
             e = launch_reas_scatter(r->dev, d_packets, stride, nPackets, sc.roWork, s, cold_loads(r, nPackets, stride));
         if (e == hipSuccess) e = note_launch(r, s);
@@ -806,9 +820,7 @@ int e2sar_hip_reas_classify(e2sar_hip_reas *r, const uint8_t *d_packets, uint32_
     hipError_t e;
     if (ref_order(r)) {
         if (int rc = ro_prepare(r, s, nPackets)) return rc;
-        const auto &sc = r->scratch[s];
-        e = launch_ro_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, sc.roScratch,
-                               sc.roScratchBytes, s);
+        e = ro_classify(r, s, d_packets, stride, d_lens, nPackets, now_ms, d_work);
     } else {
         e = launch_reas_classify(r->dev, d_packets, stride, d_lens, nPackets, now_ms, d_work, s);
     }
@@ -867,9 +879,7 @@ int e2sar_hip_reas_scatter_classify(e2sar_hip_reas *r, uint32_t stride, const ui
         e = launch_reas_scatter(r->dev, d_spk, stride, sn, d_swork, s, cold_loads(r, sn, stride));
         if (e == hipSuccess && cn) {
             if (int rc = ro_prepare(r, s, cn)) return rc;
-            const auto &sc = r->scratch[s];
-            e = launch_ro_classify(r->dev, d_cpk, stride, d_clens, cn, now_ms, d_cwork, sc.roScratch,
-                                   sc.roScratchBytes, s);
+            e = ro_classify(r, s, d_cpk, stride, d_clens, cn, now_ms, d_cwork);
         }
     } else {
         e = launch_reas_scatter_classify(r->dev, stride, d_spk, sn, d_swork, d_cpk, d_clens, cn, now_ms, d_cwork, s,

@@ -1,6 +1,7 @@
 // host_common.hpp -- internal helpers shared by the Segmenter/Reassembler façade.
 #pragma once
 
+#include <atomic>
 #include <chrono>
 #include <map>
 #include <string>
@@ -36,6 +37,8 @@ float clock_entropy_bits();
 // Segmenter MTU rules (segmenter.cpp): interface/override resolution and the 9000-byte limit
 uint32_t resolve_mtu(uint16_t flagsMtu, uint32_t ifMtu, const std::string &iface);
 void check_mtu_limit(uint32_t mtu);
+EventNum_t take_send_number(std::atomic<EventNum_t> &userEventNum, EventNum_t eventNum, size_t depth, size_t cap,
+                            bool *accepted);
 
 inline uint64_t steady_ms()
 {

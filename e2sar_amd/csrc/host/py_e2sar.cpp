@@ -246,7 +246,9 @@ PYBIND11_MODULE(e2sar_py, m)
             ccb = PyCallback::execute;
             carg = new PyCallback{cb, arg};
         }
-        return s.addToSendQueue(static_cast<uint8_t *>(bi.ptr), bytes, (EventNum_t)ev, did, ent, ccb, carg);
+        auto res = s.addToSendQueue(static_cast<uint8_t *>(bi.ptr), bytes, (EventNum_t)ev, did, ent, ccb, carg);
+        if (res.has_error() && ccb) delete std::any_cast<PyCallback *>(carg);   // refused: never called back
+        return res;
     };
     seg.def("addNumpyArrayToSendQueue", queue, py::arg("numpy_array"), py::arg("nbytes"), py::arg("_eventNum") = 0LL,
             py::arg("_dataId") = 0, py::arg("entropy") = 0, py::arg("callback") = py::none(),

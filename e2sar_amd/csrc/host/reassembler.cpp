@@ -25,6 +25,7 @@
 #include <deque>
 #include <map>
 #include <mutex>
+#include <new>
 #include <set>
 #include <thread>
 
@@ -77,14 +78,13 @@ struct Reassembler::Impl {
     std::condition_variable bFreeCv, bFullCv;
     std::deque<Batch *> freeB, fullB;
 
-    // event queue (QSIZE 1000, hpp:126) and lost events (hpp:102-122, 262-279)
+    // event queue (hpp:126-127: unbounded, see gatherFinish) and lost events (hpp:102-122, 262-279)
     struct Ev {
         uint8_t *event;
         size_t bytes;
         EventNum_t eventNum;
         uint16_t dataId;
     };
-    static constexpr size_t kQSize = 1000;
     std::mutex eMu;
     std::condition_variable eCv;
     std::deque<Ev> evq;
@@ -444,24 +444,35 @@ void Reassembler::Impl::gatherFinish(uint32_t first, uint32_t upto)
         lastErr = E2SARErrorc::SystemError;
         return;
     }
+    // The reference's eventQueue (hpp:126-127) is a boost::lockfree::queue without
+    // fixed_sized: QSIZE only pre-sizes its node pool and push() allocates past it, so an
+    // enqueue fails (hpp:138-144 -> enqueueLoss, cpp:413-421) only when allocation does.
+    // The queue here is unbounded the same way; a failed allocation is the only loss.
+    auto lose = [this](EventNum_t eventNum, uint16_t dataId) {
+        hostEnqueueLoss++;
+        std::lock_guard<std::mutex> l2(lMu);
+        if (lostSeen.insert({eventNum, dataId}).second) lostq.emplace_back(eventNum, dataId, 0);
+    };
     std::vector<Ev> ready;
     ready.reserve(upto - first);
     for (uint32_t k = first; k < upto; k++) {
         const auto &r = recs[k];
-        auto *buf = new uint8_t[r.bytes ? r.bytes : 1];
+        auto *buf = new (std::nothrow) uint8_t[r.bytes ? r.bytes : 1];
+        if (!buf) {
+            lose(r.eventNum, r.dataId);
+            continue;
+        }
         if (r.bytes) memcpy(buf, stage + stageOffs[k - first], r.bytes);
         ready.push_back(Ev{buf, r.bytes, r.eventNum, r.dataId});
     }
     {
         std::lock_guard<std::mutex> lk(eMu);
         for (auto &e : ready) {
-            if (evq.size() >= kQSize) {                  // enqueue loss (hpp:140-145, cpp:413-421)
-                hostEnqueueLoss++;
-                std::lock_guard<std::mutex> l2(lMu);
-                if (lostSeen.insert({e.eventNum, e.dataId}).second) lostq.emplace_back(e.eventNum, e.dataId, 0);
-                delete[] e.event;
-            } else {
+            try {
                 evq.push_back(e);
+            } catch (const std::bad_alloc &) {
+                lose(e.eventNum, e.dataId);
+                delete[] e.event;
             }
         }
     }

@@ -157,6 +157,19 @@ void check_mtu_limit(uint32_t mtu)
 {
     if (mtu > 9000) throw E2SARException("MTU set too long, limit 9000");
 }
+
+// addToSendQueue's numbering (cpp:925-937): an explicit number resets the counter, and the
+// number is taken before the push can fail (cpp:939-946), so a refused default-numbered
+// event leaves a gap.  Returns the number taken; *accepted says whether a queue holding
+// `depth` items of `cap` takes the event.
+EventNum_t take_send_number(std::atomic<EventNum_t> &userEventNum, EventNum_t eventNum, size_t depth, size_t cap,
+                            bool *accepted)
+{
+    if (eventNum != 0) userEventNum.exchange(eventNum);
+    const EventNum_t num = userEventNum++;
+    *accepted = depth < cap;
+    return num;
+}
 }  // namespace detail
 
 // e2sarDPSegmenter.hpp:298-317 + ctor checks at cpp:52-53
@@ -577,12 +590,13 @@ result<int> Segmenter::addToSendQueue(uint8_t *event, size_t bytes, EventNum_t _
                                       uint16_t entropy, void (*callback)(std::any), std::any cbArg) noexcept
 {
     auto &m = *impl;
-    if (_eventNum != 0) m.userEventNum.exchange(_eventNum);
     try {
         std::lock_guard<std::mutex> lk(m.qMu);
-        if (m.q.size() >= Impl::kQueueCap)
+        bool accepted;
+        const EventNum_t num = detail::take_send_number(m.userEventNum, _eventNum, m.q.size(), Impl::kQueueCap, &accepted);
+        if (!accepted)
             return E2SARErrorInfo{E2SARErrorc::MemoryError, "Send queue is temporarily full, try again later"};
-        m.q.push_back(Impl::Item{event, bytes, m.userEventNum++, (uint16_t)(_dataId == 0 ? m.dataId : _dataId),
+        m.q.push_back(Impl::Item{event, bytes, num, (uint16_t)(_dataId == 0 ? m.dataId : _dataId),
                                  entropy, callback, std::move(cbArg)});
     } catch (const std::exception &e) {
         return E2SARErrorInfo{E2SARErrorc::CaughtException, e.what()};

@@ -246,17 +246,24 @@ class SpreadPipeline:
        the Infinity Cache;
     2. the foreign ones are appended to per-owner regions (``RegionRouter``, one launch);
 
-    then, on a count stream of its own and through a communicator of its own, the per-owner
-    counts are all-gathered (RCCL) and copied to pinned host memory.  The host reads batch
-    b's counts only after it has queued batch b + depth - 1's landing work -- by then they
-    have long arrived (the count stream never queues behind an exchange), so the host never
-    waits for the GPU -- then issues batch b's ``all_to_all`` of the regions (RCCL, peer to
-    peer over xGMI) on the communication stream and the reassembly of what arrived (classify
-    + scatter with streaming loads) on a third stream.  So batch b's exchange and the
-    reassembly of what it brought run while later batches land and are reassembled in
+    then, on the communication stream, the per-owner counts are all-gathered (RCCL) and
+    copied to pinned host memory.  The host reads batch b's counts only after it has queued
+    batch b + depth - 1's landing work, then issues batch b's ``all_to_all`` of the regions
+    (RCCL, peer to peer over xGMI) on the same stream and the reassembly of what arrived
+    (classify + scatter with streaming loads) on a second stream.  So batch b's exchange and
+    the reassembly of what it brought run while later batches land and are reassembled in
     place, and the step costs max(landing, exchange) instead of their sum.  ``depth``
     region / receive buffer sets rotate; a set is reused only after the exchange and
     reassembly that read it have finished (stream events, no host wait).
+
+    Every collective -- count all-gathers and exchanges alike -- goes through ONE
+    communicator on ONE stream, in one order that every rank issues identically (each
+    land(): the exchange of batch b - depth + 1, then the count gather of batch b).  RCCL,
+    like NCCL, does not promise progress for collectives of two communicators in flight at
+    once, so nothing here depends on it: the stream serialises the collectives in the order
+    every rank enqueued them.  The cost is that batch b's count gather queues behind batch
+    b - depth + 1's exchange, so the host, reading b's counts depth - 1 landings later,
+    waits only when the exchange has fallen depth - 1 batches behind the landing.
 
     With gloo (the CPU / one-GPU rehearsal) every exchange is synchronous through host
     memory and the received datagrams are reassembled on the caller's stream.
@@ -267,12 +274,10 @@ class SpreadPipeline:
 
     def __init__(self, ctx, R, stride: int, max_batch: int, world: int, rank: int,
                  group: Optional[dist.ProcessGroup] = None, depth: int = 3, with_lb_header: bool = True,
-                 in_place: bool = True, count_group: Optional[dist.ProcessGroup] = None):
+                 in_place: bool = True):
         """in_place=False routes every landed datagram, this rank's own included, through the
         exchange (no in-place reassembly): the route-all form, which also drives the whole
-        RCCL data path at world 1.  With RCCL the count all-gathers run through a second
-        communicator (count_group, or one created here -- a collective call: every rank
-        constructs its pipeline at the same point), so they never queue behind an exchange."""
+        RCCL data path at world 1."""
         if depth < 2:
             # a region set is reused only after the exchange that reads it was issued, which
             # happens one land() later: with one set, land() would reset and refill it under
@@ -293,11 +298,6 @@ class SpreadPipeline:
         self.work = [R.alloc_work(rcap) for _ in range(depth)] if self.active else []
         self.comm = torch.cuda.Stream(dev) if self.nccl else None
         self.rx = torch.cuda.Stream(dev) if self.nccl else None
-        self.cstream = torch.cuda.Stream(dev) if self.nccl else None
-        if self.nccl and count_group is None:
-            count_group = dist.new_group(ranks=list(range(dist.get_world_size(group))), backend="nccl",
-                                         device_id=dev)
-        self.cgroup = count_group
         self.lag = depth - 1                  # batches whose exchange is still to be issued
         self.mat_dev = [torch.zeros(world * world, dtype=torch.int32, device=dev) for _ in range(depth)]
         self.mat_host = [torch.zeros(world * world, dtype=torch.int32).pin_memory() for _ in range(depth)] \
@@ -344,15 +344,15 @@ class SpreadPipeline:
             self._exchange_sync(slot, main)
             return
         self.ev_routed[slot].record(main)
-        # exchange the batch landed depth - 1 batches ago (its counts are on the host by now);
-        # every rank issues each communicator's collectives in the same order
+        # exchange the batch landed depth - 1 batches ago, then gather this batch's counts:
+        # both on the one communication stream and communicator, in this order on every rank
         while len(self.pending) >= self.lag:
             self._finish(self.pending.pop(0))
-        with torch.cuda.stream(self.cstream):
-            self.cstream.wait_event(self.ev_routed[slot])
-            dist.all_gather_into_tensor(self.mat_dev[slot], router.running, group=self.cgroup)
+        with torch.cuda.stream(self.comm):
+            self.comm.wait_event(self.ev_routed[slot])
+            dist.all_gather_into_tensor(self.mat_dev[slot], router.running, group=self.group)
             self.mat_host[slot].copy_(self.mat_dev[slot], non_blocking=True)
-            self.ev_cnt[slot].record(self.cstream)
+            self.ev_cnt[slot].record(self.comm)
         self.pending.append(slot)
 
     def _counts(self, m: List[List[int]]):
@@ -366,9 +366,9 @@ class SpreadPipeline:
 
     def _finish(self, slot: int) -> None:
         """Batch of region set `slot`: read its counts (host), exchange, reassemble arrivals.
-        Called depth - 1 batches after the batch landed, so the wait below finds the counts
-        already there (a rank only blocks here if the GPU is more than depth - 1 batches
-        behind the host)."""
+        Called depth - 1 batches after the batch landed; its count gather was queued behind
+        the exchange issued depth - 1 batches before it, so the wait below blocks only while
+        the exchanges run more than depth - 1 batches behind the landing."""
         self.ev_cnt[slot].synchronize()
         flat = self.mat_host[slot].tolist()
         W = self.world
@@ -425,4 +425,3 @@ class SpreadPipeline:
             main = torch.cuda.current_stream()
             main.wait_stream(self.comm)
             main.wait_stream(self.rx)
-            main.wait_stream(self.cstream)

@@ -7,6 +7,7 @@
  */
 #include "e2sar_oracle.h"
 
+#include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
 
@@ -179,7 +180,12 @@ e2o_reas *e2o_reas_new(int withLBHeader, size_t queueCapacity)
 {
     e2o_reas *r = (e2o_reas *)calloc(1, sizeof(e2o_reas));
     r->withLB = withLBHeader;
-    r->qcap = queueCapacity ? queueCapacity : 1000;   /* QSIZE{1000} (hpp:126) */
+    /* The reference's eventQueue{QSIZE} (hpp:126-127) is a boost::lockfree::queue WITHOUT
+     * fixed_sized: QSIZE pre-sizes its node pool, push() allocates beyond it, so an enqueue
+     * fails only on allocation failure -- the queue is unbounded.  queueCapacity 0 restates
+     * that; a nonzero capacity models the device's completed-record ring
+     * (e2sar_hip_reas_config.queueCapacity), a parameter of this build, not of the reference. */
+    r->qcap = queueCapacity ? queueCapacity : SIZE_MAX;
     return r;
 }
 
@@ -293,7 +299,7 @@ void e2o_reas_push(e2o_reas *r, const uint8_t *dgram, size_t nbytes)
         *slot = it->next;                        /* erase (:409) */
         it->next = NULL;
         r->inProgress--;
-        if (r->qlen >= r->qcap) {                /* enqueue failed (hpp:140-145) */
+        if (r->qlen >= r->qcap) {                /* device ring full (hpp:140-145's failure path) */
             log_lost(r, it, 1);
             free_item(it);
         } else {

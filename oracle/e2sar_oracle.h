@@ -69,6 +69,8 @@ typedef struct e2o_reas_stats {
     uint64_t inProgress;         /* size of eventsInProgress */
 } e2o_reas_stats;
 
+/* queueCapacity 0 = the reference's unbounded eventQueue (hpp:126-127); nonzero models the
+ * device's completed-record ring (a build parameter, not reference behaviour) */
 e2o_reas *e2o_reas_new(int withLBHeader, size_t queueCapacity);
 void e2o_reas_free(e2o_reas *r);
 /* logical clock (ms) used for firstSegment / GC (stands in for steady_clock) */

@@ -61,15 +61,21 @@ def full_case(name, payload, mtu, ver, event_num, data_id, entropy, tick):
             "datagrams_hex": [pk[k, : int(ln[k])].tobytes().hex() for k in range(len(ln))]}
 
 
-def reas_case(name, dgrams, with_lb, qcap=1000):
-    r = O.Reassembler(with_lb, qcap)
+def reas_case(name, dgrams, with_lb, ring=0):
+    """ring 0: the reference's unbounded eventQueue (hpp:126-127); ring > 0: the device's
+    completed-record ring of that capacity (e2sar_hip_reas_config.queueCapacity), a
+    parameter of this build -- not reference behaviour"""
+    r = O.Reassembler(with_lb, ring)
     for d in dgrams:
         r.push(d)
     evs = r.pop_all()
-    return {"name": name, "withLBHeader": with_lb,
+    c = {"name": name, "withLBHeader": with_lb,
             "datagrams_hex": [d.hex() for d in dgrams],
             "events": [{"eventNum": e, "dataId": d, "hex": b.hex()} for b, e, d in evs],
             "stats": r.stats()}
+    if ring:
+        c["deviceRingCapacity"] = ring
+    return c
 
 
 def main():
@@ -109,7 +115,7 @@ def main():
     g["reassemble"].append(reas_case("mtu80_bad_version_lb", badv, True))
     nolb = [d[16:] for d in dg[0]]
     g["reassemble"].append(reas_case("mtu80_no_lb_header", nolb, False))
-    g["reassemble"].append(reas_case("mtu80_queue_full_lb", in_order, True, qcap=2))
+    g["reassemble"].append(reas_case("mtu80_device_ring_cap2_lb", in_order, True, ring=2))
 
     path = os.path.join(HERE, "sar_golden.json")
     with open(path, "w") as f:

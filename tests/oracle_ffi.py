@@ -121,7 +121,9 @@ def segment_event(event: np.ndarray, event_num: int, data_id: int, entropy: int,
 class Reassembler:
     """The reference recv body restated (e2sarDPReassembler.cpp:310-428)."""
 
-    def __init__(self, with_lb_header: bool, queue_capacity: int = 1000):
+    def __init__(self, with_lb_header: bool, queue_capacity: int = 0):
+        """queue_capacity 0: the reference's unbounded eventQueue (hpp:126-127); nonzero: a
+        device completed-record ring of that capacity (not reference behaviour)"""
         self.h = lib().e2o_reas_new(int(with_lb_header), queue_capacity)
 
     def set_time(self, ms: int):

@@ -604,3 +604,71 @@ def test_mtu_auto_detect_from_the_outgoing_interface(E):
         make_seg(E, port, mtu=0)
     seg2 = make_seg(E, port, mtu=1500)
     assert seg2.getIntf() == "lo" and seg2.getMTU() == 1500
+
+
+# ------------------------------- queue capacities -------------
+
+def test_event_queue_is_unbounded_2000_events_undrained(E):
+    """The reference's receive queue is boost::lockfree::queue<EventQueueItem*>{QSIZE} without
+    fixed_sized (e2sarDPReassembler.hpp:126-127): QSIZE (1000) pre-sizes its node pool and
+    push() allocates beyond it, so a caller that drains late still gets every event and
+    enqueueLoss stays 0.  2000 events are sent and reassembled before anything is drained."""
+    port = next_port()
+    reas = make_reas(E, port)
+    ok(reas.OpenAndStart())
+    seg = make_seg(E, port, mtu=1500, sockets=1)
+    ok(seg.OpenAndStart())
+    n = 2000
+    rng = np.random.default_rng(20002)
+    payloads = [rng.integers(0, 256, 200 + (i * 37) % 3000, dtype=np.uint8).tobytes() for i in range(n)]
+    for k, p in enumerate(payloads):
+        ok(seg.sendEvent(p, len(p)))
+        if k % 200 == 199:
+            time.sleep(0.02)                 # keep the loopback socket buffer from overflowing
+    deadline = time.time() + 30
+    while time.time() < deadline and reas.getStats().eventSuccess < n:
+        time.sleep(0.05)
+    st = reas.getStats()
+    assert st.eventSuccess == n and st.enqueueLoss == 0 and st.reassemblyLoss == 0, \
+        (st.eventSuccess, st.enqueueLoss, st.reassemblyLoss)
+    got = {}
+    for _ in range(n):
+        ln, data, ev, did = reas.getEventBytes()
+        assert ln >= 0 and did == DATA_ID
+        got[ev] = data
+    assert reas.getEventBytes()[0] == -1
+    assert sorted(got) == list(range(n))
+    assert all(got[k] == payloads[k] for k in range(n))
+    assert reas.getStats().enqueueLoss == 0 and reas.get_LostEvent() == ()
+    seg.stopThreads()
+    reas.stopThreads()
+
+
+def test_send_queue_full_consumes_an_event_number(E):
+    """addToSendQueue takes userEventNum++ before the push can fail (e2sarDPSegmenter.cpp:
+    937, 939-946): with the queue full (2047 items, hpp:101) the refused default-numbered
+    event still uses up its number, so the next accepted event skips it."""
+    port = next_port()
+    cap = 2047
+    t, got = capture(port, cap + 1, timeout=10.0)
+    seg = make_seg(E, port, mtu=1500, sockets=1)
+    bufs = [bytes([k & 0xFF]) * 64 for k in range(cap + 2)]    # kept alive until sent
+    for k in range(cap):                     # not started yet: nothing drains the queue
+        ok(seg.addToSendQueue(bufs[k], len(bufs[k])))
+    r = seg.addToSendQueue(bufs[cap], len(bufs[cap]))
+    assert r.has_error()                     # MemoryError, "Send queue is temporarily full"
+    ok(seg.OpenAndStart())
+    deadline = time.time() + 20                # let the send thread drain the queue (a retry
+    while time.time() < deadline and seg.getSendStats().msgCnt < cap:   # would consume numbers too)
+        time.sleep(0.01)
+    ok(seg.addToSendQueue(bufs[cap + 1], len(bufs[cap + 1])))
+    seg.stopThreads()                        # drains the queue first
+    t.join()
+    assert len(got) == cap + 1
+    evs = {}
+    for d in got:
+        okv, did, off, blen, ev, _ = O.re_parse(d[16:36])
+        assert okv and did == DATA_ID and off == 0 and blen == 64
+        evs[ev] = d[36:]
+    assert sorted(evs) == list(range(cap)) + [cap + 1]        # number `cap` was consumed
+    assert evs[cap + 1] == bufs[cap + 1] and evs[0] == bufs[0] and evs[cap - 1] == bufs[cap - 1]

@@ -99,7 +99,8 @@ def _reas_case(ctx, case, mode, per_datagram, flags=0):
         lens[k] = len(d)
     dpk = torch.from_numpy(host.reshape(-1)).to(ctx.torch_device)
     dln = torch.from_numpy(lens.view(np.int32)).to(ctx.torch_device)
-    qcap = 2 if case["name"].endswith("queue_full_lb") else 1000
+    # the device's completed-record ring; the reference's queue is unbounded (hpp:126-127)
+    qcap = case.get("deviceRingCapacity", 1000)
     R = sar.DeviceReassembler(ctx, with_lb_header=case["withLBHeader"], table_slots=64, queue_capacity=qcap,
                               lost_capacity=64, arena_bytes=1 << 16, flags=flags)
     spans = [(k, k + 1) for k in range(len(dg))] if per_datagram else [(0, len(dg))]
@@ -143,8 +144,8 @@ def test_golden_reassembly_cases(hip, golden, mode, per_datagram):
             assert st["eventSuccess"] == 1 and st["inProgress"] == 0
             assert st["totalPackets"] == exp["totalPackets"] and st["totalBytes"] == exp["totalBytes"]
             continue
-        if name.endswith("queue_full_lb") and not per_datagram:
-            # three events complete in one launch: which two fit the 2-record queue is the
+        if case.get("deviceRingCapacity") and not per_datagram:
+            # three events complete in one launch: which two fit the 2-record ring is the
             # device's completion order; counts and bytes still match
             assert st == exp, name
             assert len(got) == 2 and all(got[k] == h for k, h in _expected(case).items() if k in got)

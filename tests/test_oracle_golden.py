@@ -143,8 +143,7 @@ def test_fixture_segment_digests(golden):
 
 def test_fixture_reassembly(golden):
     for c in golden["reassemble"]:
-        qcap = 2 if c["name"].endswith("queue_full_lb") else 1000
-        r = O.Reassembler(c["withLBHeader"], qcap)
+        r = O.Reassembler(c["withLBHeader"], c.get("deviceRingCapacity", 0))
         for d in c["datagrams_hex"]:
             r.push(bytes.fromhex(d))
         evs = [{"eventNum": e, "dataId": d, "hex": b.hex()} for b, e, d in r.pop_all()]
@@ -158,6 +157,25 @@ def test_fixture_quirks_documented(golden):
     assert by["mtu80_late_offset0_quirk_lb"]["stats"]["eventSuccess"] == 0
     # a duplicate fragment is double counted: curBytes overshoots, never == bytes (cpp:400-403)
     assert by["mtu80_duplicate_fragment_lb"]["stats"]["eventSuccess"] == 0
-    # enqueue loss still counts eventSuccess (cpp:413-426)
-    st = by["mtu80_queue_full_lb"]["stats"]
+    # a record lost to a full device ring still counts eventSuccess, as an enqueue loss does
+    # in the reference (cpp:413-426); the ring's capacity is this build's parameter
+    st = by["mtu80_device_ring_cap2_lb"]["stats"]
     assert st["eventSuccess"] == 3 and st["enqueueLoss"] == 1
+
+
+def test_oracle_event_queue_is_unbounded():
+    """The reference's eventQueue{QSIZE} (e2sarDPReassembler.hpp:126-127) is a
+    boost::lockfree::queue without fixed_sized: push() allocates beyond QSIZE (1000), so a
+    receiver drained late still delivers every event with enqueueLoss == 0."""
+    mp = O.max_pld_len(80)
+    r = O.Reassembler(True)
+    n = 2000
+    evs = [S.event_bytes(7 + i, 67 + (i % 5)) for i in range(n)]
+    for i, ev in enumerate(evs):
+        pk, ln = O.segment_event(ev, i, 4321, 7, 99, 2, mp)
+        for k in range(len(ln)):
+            r.push(pk[k, : int(ln[k])].tobytes())
+    got = r.pop_all(cap=256)
+    st = r.stats()
+    assert st["enqueueLoss"] == 0 and st["eventSuccess"] == n and len(got) == n
+    assert all(b == evs[e].tobytes() for b, e, d in got)

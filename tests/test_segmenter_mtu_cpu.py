@@ -67,3 +67,53 @@ def test_resolved_mtu_above_9000_is_refused(tmp_path):
     assert "limit 9000" in got[(9216, 65520)]
     assert "exceeds outgoing interface MTU" in got[(9000, 1500)]
     assert got[(1500, 0)] == "ok 1500"
+
+
+NUMBERING = r"""
+#include <atomic>
+#include <cstdio>
+#include "e2sar_amd/e2sar.hpp"
+namespace e2sar { namespace detail {
+EventNum_t take_send_number(std::atomic<EventNum_t> &userEventNum, EventNum_t eventNum, size_t depth, size_t cap,
+                            bool *accepted);
+} }
+int main()
+{
+    // a send queue of capacity 3 (the facade's is 2047, e2sarDPSegmenter.hpp:101)
+    std::atomic<e2sar::EventNum_t> num{0};
+    size_t depth = 0;
+    auto push = [&](e2sar::EventNum_t ev) {
+        bool ok;
+        const auto n = e2sar::detail::take_send_number(num, ev, depth, 3, &ok);
+        if (ok) depth++;
+        printf("%llu %d\n", (unsigned long long)n, ok ? 1 : 0);
+    };
+    push(0); push(0); push(0);        // 0 1 2 queued
+    push(0);                          // 3 refused: the number is consumed anyway
+    depth--;                          // the send thread takes one
+    push(0);                          // 4 queued: 3 is a gap
+    push(0);                          // 5 refused
+    depth = 0;
+    push(100);                        // explicit number resets the counter
+    push(0);                          // 101
+    return 0;
+}
+"""
+
+
+def test_send_queue_numbering_under_a_full_queue(tmp_path):
+    """addToSendQueue takes userEventNum++ before the push can fail (e2sarDPSegmenter.cpp:
+    937 before 939-946), so a refused default-numbered event leaves a gap in the numbering;
+    an explicit event number resets the counter first (cpp:926-927)."""
+    if not os.path.exists(os.path.join(LIB, "libe2sar_amd.so")):
+        pytest.skip("libe2sar_amd.so not built")
+    src = tmp_path / "num.cpp"
+    src.write_text(NUMBERING)
+    exe = tmp_path / "num"
+    r = subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe),
+                        "-L", LIB, "-le2sar_amd", "-le2sar_hip", f"-Wl,-rpath,{LIB}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    out = [tuple(map(int, l.split())) for l in
+           subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.splitlines()]
+    assert out == [(0, 1), (1, 1), (2, 1), (3, 0), (4, 1), (5, 0), (100, 1), (101, 1)]

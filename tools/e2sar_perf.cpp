@@ -33,8 +33,10 @@ namespace {
 
 std::atomic<size_t> sharedReceived{0};   // events received by all dequeue threads
 
-const std::string kHead = "[e2sar_perf event head]";
-const std::string kTail = "[e2sar_perf event tail]";
+// the reference tool's event payload markers (bin/e2sar_perf.cpp:27-28), so the two tools
+// fill events with the same bytes
+const std::string kHead = "This is a start of event payload";
+const std::string kTail = "...the end";
 
 struct Opts {
     bool send = false, recv = false, loopback = false, quiet = false;

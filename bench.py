@@ -87,6 +87,9 @@ def parse(argv=None):
     ap.add_argument("--roofline-steps", type=int, default=2)
     ap.add_argument("--landing", choices=["own", "spread"], default="own",
                     help="own: datagrams land on their owner; spread: owners spread, RCCL exchange (config 4)")
+    ap.add_argument("--fold-recycle", type=int, default=1,
+                    help="1: the step's table/arena recycle runs inside its first seg_kernel launch "
+                         "(e2sar_hip_segment_batch_recycle); 0: a reas_recycle_kernel launch of its own")
     ap.add_argument("--reas-group", type=int, default=0,
                     help="A/B: datagrams per fused-reassembly workgroup (1..64; 0 = the library's balanced choice)")
     ap.add_argument("--table-factor", type=int, default=8,
@@ -629,7 +632,11 @@ def run_workload(args, env, headline: bool):
         s0 = torch.cuda.current_stream()
         if spread:
             return step_spread()
-        R.recycle(force=True)
+        # the default step recycles in its first segmentation launch (extra workgroups at the
+        # end of seg_kernel's grid, e2sar_hip_segment_batch_recycle): one launch fewer per step
+        fold = args.fold_recycle and args.reas in ("fused", "split") and not args.overlap and args.lanes == 1
+        if not fold:
+            R.recycle(force=True)
         if args.reas == "pipelined":
             # seg(0), classify(0); then per batch: seg(b+1), [scatter(b) | classify(b+1)]
             # in one launch; buffers b%2 are rewritten by seg(b+2) after that launch.
@@ -668,7 +675,10 @@ def run_workload(args, env, headline: bool):
         if not args.overlap:
             for k, p in enumerate(plans):
                 pk, ln = bufs[k % nbuf] if args.lanes > 1 else bufs[0]
-                timed("seg_kernel", seg.segment, p, pk, ln)
+                if k == 0 and fold:
+                    timed("seg_kernel", seg.segment, p, pk, ln, recycle=R, force=True)
+                else:
+                    timed("seg_kernel", seg.segment, p, pk, ln)
                 reassemble(pk, ln, p.total_packets, k)
             return
         s1 = side

@@ -164,6 +164,7 @@ SIGNATURES = {
     "e2sar_hip_seg_plan": (i, [C.POINTER(SegEvent), u32, sz, C.POINTER(u32), C.POINTER(u32)]),
     "e2sar_hip_segment_batch": (i, [vp, vp, u32, u32, i, u32, i, vp, u32, vp, vp]),
     "e2sar_hip_segment_batch_dev": (i, [vp, vp, vp, u32, u32, i, u32, vp, u32, vp, vp]),
+    "e2sar_hip_segment_batch_recycle": (i, [vp, vp, u32, u32, i, u32, i, vp, u32, vp, vp, i, vp]),
     "e2sar_hip_relay_plan": (i, [vp, u32, u32, sz, u64, C.c_uint16, vp, vp, vp]),
     "e2sar_hip_reas_create": (i, [vp, C.POINTER(ReasConfig), C.POINTER(vp)]),
     "e2sar_hip_reas_destroy": (None, [vp]),

@@ -1056,23 +1056,56 @@ int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out)
     return E2SAR_HIP_OK;
 }
 
+// e2sar_hip_reas_recycle's precondition (caller holds r->mu): without force, the device
+// is drained and no event is in progress or unpolled
+static int recycle_check(e2sar_hip_reas *r, int force, hipStream_t s)
+{
+    if (force) return E2SAR_HIP_OK;
+    ReasCtl c;
+    if (int rc = wait_launches(r)) return rc;
+    HIP_TRY(hipStreamSynchronize(s));
+    if (int rc = read_ctl_occ(r, c)) return rc;
+    if (c.inProgress != 0) return fail(E2SAR_HIP_ERR_LOGIC, "events still in progress");
+    if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
+    return E2SAR_HIP_OK;
+}
+
 int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream)
 {
     if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
     std::lock_guard<std::mutex> lk(r->mu);
     HIP_TRY(hipSetDevice(r->ctx->device));
     hipStream_t s = stream ? static_cast<hipStream_t>(stream) : r->ctx->stream;
-    if (!force) {
-        ReasCtl c;
-        if (int rc = wait_launches(r)) return rc;
-        HIP_TRY(hipStreamSynchronize(s));
-        if (int rc = read_ctl_occ(r, c)) return rc;
-        if (c.inProgress != 0) return fail(E2SAR_HIP_ERR_LOGIC, "events still in progress");
-        if (c.nCompleted != 0) return fail(E2SAR_HIP_ERR_LOGIC, "completed events not yet polled");
-    }
+    if (int rc = recycle_check(r, force, s)) return rc;
     hipError_t e = launch_recycle(r->dev, force != 0, s);
     if (e == hipSuccess) e = note_launch(r, s);
     if (e != hipSuccess) return hip_fail(e, "recycle launch");
+    return E2SAR_HIP_OK;
+}
+
+int e2sar_hip_segment_batch_recycle(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, uint32_t nEvents,
+                                    uint32_t maxPacketsPerEvent, int lbHdrVersion, uint32_t maxPldLen,
+                                    int eventsDwordAligned, uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
+                                    e2sar_hip_reas *r, int force, void *stream)
+{
+    if (!ctx) return fail(E2SAR_HIP_ERR_PARAMETER, "ctx is NULL");
+    if (!r) return fail(E2SAR_HIP_ERR_PARAMETER, "reas is NULL");
+    if (r->ctx->device != ctx->device) return fail(E2SAR_HIP_ERR_PARAMETER, "reassembler on another device");
+    if (nEvents && (!d_events || !d_packets)) return fail(E2SAR_HIP_ERR_PARAMETER, "NULL device buffer");
+    if (maxPldLen == 0) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen is 0 (MTU too small)");
+    if (maxPldLen > 65535u) return fail(E2SAR_HIP_ERR_PARAMETER, "maxPldLen above a UDP datagram");
+    if ((stride & 15u) || stride < E2SAR_HIP_LBRE_HDR_LEN + maxPldLen)
+        return fail(E2SAR_HIP_ERR_PARAMETER, "stride must be a multiple of 16 and hold 36 + maxPldLen");
+    if (((uintptr_t)d_packets & 15u) != 0) return fail(E2SAR_HIP_ERR_PARAMETER, "packet buffer not 16-byte aligned");
+    (void)eventsDwordAligned;
+    std::lock_guard<std::mutex> lk(r->mu);
+    HIP_TRY(hipSetDevice(ctx->device));
+    hipStream_t s = stream ? static_cast<hipStream_t>(stream) : ctx->stream;
+    if (int rc = recycle_check(r, force, s)) return rc;
+    hipError_t e = launch_segment(d_events, nEvents, maxPacketsPerEvent, lbHdrVersion, maxPldLen, d_packets, stride,
+                                  d_lens, s, nullptr, &r->dev, force != 0);
+    if (e == hipSuccess) e = note_launch(r, s);
+    if (e != hipSuccess) return hip_fail(e, "seg_kernel + recycle launch");
     return E2SAR_HIP_OK;
 }
 

@@ -431,15 +431,26 @@ __device__ __forceinline__ void seg_block(const e2sar_hip_seg_event *__restrict_
 // that wrote it, which reads measurably faster than lines another XCD wrote, also from
 // the Infinity Cache.  Units are numbered e * blocksPerEvent + bx as
 // without stripes; units past nUnits exit.
+__device__ void recycle_slots(const ReasDev &R, uint32_t s, int dropCompleted);
+
+// recMode != 0 (e2sar_hip_segment_batch_recycle): workgroups from nSegBlocks on recycle the
+// reassembler `rec` (reas_recycle_kernel's work; 2 = also drop completed records) instead of
+// segmenting.  They run at the end of the launch, in the slots the last seg blocks free; no
+// seg block touches the table, and the reassembly that used it ran before this launch.
 template <int U>
 __global__ __launch_bounds__(kSegBlock) void seg_kernel(const e2sar_hip_seg_event *__restrict__ events,
                                                               uint32_t blocksPerEvent, int lbVersion,
                                                               uint32_t maxPld, uint8_t *__restrict__ pkts,
                                                               uint32_t stride, uint32_t *__restrict__ lens,
                                                               const uint32_t *__restrict__ dCount, uint32_t stripe,
-                                                              uint32_t nUnits)
+                                                              uint32_t nUnits, ReasDev rec, uint32_t nSegBlocks,
+                                                              int recMode)
 {
     uint32_t blk = blockIdx.x;
+    if (recMode && blk >= nSegBlocks) {
+        recycle_slots(rec, (blk - nSegBlocks) * kSegBlock + threadIdx.x, recMode == 2);
+        return;
+    }
     if (stripe) {
         const uint32_t x = blk & 7u, k = blk >> 3;
         blk = ((k / stripe) * 8u + x) * stripe + k % stripe;
@@ -2240,9 +2251,8 @@ __global__ __launch_bounds__(kBlock) void reas_gc_kernel(ReasDev R, uint64_t now
     }
 }
 
-__global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dropCompleted)
+__device__ void recycle_slots(const ReasDev &R, uint32_t s, int dropCompleted)
 {
-    const uint32_t s = blockIdx.x * kBlock + threadIdx.x;
     if (s < R.tableSlots) {
         ReasSlot z{};
         R.slots[s] = z;
@@ -2257,6 +2267,11 @@ __global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dro
         *occ_in_progress(R, s) = 0ull;
         *occ_table_used(R, s) = 0ull;
     }
+}
+
+__global__ __launch_bounds__(kBlock) void reas_recycle_kernel(ReasDev R, int dropCompleted)
+{
+    recycle_slots(R, blockIdx.x * kBlock + threadIdx.x, dropCompleted);
 }
 
 // Compaction: one block per slot of `from`.  Surviving (READY) events get a new buffer
@@ -2409,21 +2424,27 @@ static bool seg_geom(uint32_t nEvents, uint32_t maxPacketsPerEvent, uint32_t str
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           uint8_t *pkts, uint32_t stride, uint32_t *lens,
-                          hipStream_t stream, const uint32_t *d_count)
+                          hipStream_t stream, const uint32_t *d_count, const ReasDev *rec, bool dropCompleted)
 {
-    if (nEvents == 0 || maxPacketsPerEvent == 0) return hipSuccess;
+    if (nEvents == 0 || maxPacketsPerEvent == 0) return rec ? launch_recycle(*rec, dropCompleted, stream) : hipSuccess;
     SegGeom sg;
     if (!seg_geom(nEvents, maxPacketsPerEvent, stride, sg)) return hipErrorInvalidValue;
-    const uint64_t grid = sg.stripe ? (sg.nUnits + 8ull * sg.stripe - 1) / (8ull * sg.stripe) * 8ull * sg.stripe
-                                    : sg.nUnits;
+    const uint64_t segGrid = sg.stripe ? (sg.nUnits + 8ull * sg.stripe - 1) / (8ull * sg.stripe) * 8ull * sg.stripe
+                                       : sg.nUnits;
+    const uint64_t grid = segGrid + (rec ? cdiv(rec->tableSlots > kShards ? rec->tableSlots : (uint32_t)kShards,
+                                                (uint32_t)kSegBlock) : 0u);
     if (grid > 0x7FFFFFFFull) return hipErrorInvalidValue;
+    const ReasDev none{};
+    const ReasDev &rj = rec ? *rec : none;
+    const int mode = rec ? (dropCompleted ? 2 : 1) : 0;
     if (sg.U == 2)
         hipLaunchKernelGGL((seg_kernel<2>), dim3((uint32_t)grid), dim3(kSegBlock), 0, stream, d_events,
-                           sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits);
+                           sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe, (uint32_t)sg.nUnits, rj,
+                           (uint32_t)segGrid, mode);
     else
         hipLaunchKernelGGL((seg_kernel<4>), dim3((uint32_t)grid), dim3(kSegBlock), occupancy_lds(seg_kernel<4>, kSeg4PerCU),
                            stream, d_events, sg.bpe, lbVersion, maxPld, pkts, stride, lens, d_count, sg.stripe,
-                           (uint32_t)sg.nUnits);
+                           (uint32_t)sg.nUnits, rj, (uint32_t)segGrid, mode);
     return hipGetLastError();
 }
 

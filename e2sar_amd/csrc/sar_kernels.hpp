@@ -207,7 +207,8 @@ hipError_t launch_copy_spans(const CopySpans &cs, uint64_t largest, hipStream_t 
 hipError_t launch_segment(const e2sar_hip_seg_event *d_events, uint32_t nEvents,
                           uint32_t maxPacketsPerEvent, int lbVersion, uint32_t maxPld,
                           uint8_t *pkts, uint32_t stride, uint32_t *lens,
-                          hipStream_t stream, const uint32_t *d_count = nullptr);
+                          hipStream_t stream, const uint32_t *d_count = nullptr, const ReasDev *rec = nullptr,
+                          bool dropCompleted = false);
 hipError_t launch_relay_plan(const ReasDev &R, uint32_t first, uint32_t maxEvents, uint32_t maxPld,
                              uint64_t lbTick, uint32_t entropyBase, e2sar_hip_seg_event *d_events,
                              uint32_t *d_counts, hipStream_t stream);

@@ -158,15 +158,21 @@ class DeviceSegmenter:
         return pk, ln
 
     def segment(self, plan: SegPlan, packets: torch.Tensor, lens: Optional[torch.Tensor],
-                stream: Optional[torch.cuda.Stream] = None) -> int:
+                stream: Optional[torch.cuda.Stream] = None, recycle: Optional["DeviceReassembler"] = None,
+                force: bool = False) -> int:
+        """recycle: also recycle that reassembler (as DeviceReassembler.recycle(force)) in the
+        same launch (e2sar_hip_segment_batch_recycle)."""
         if packets.numel() < plan.total_packets * self.stride:
             raise ValueError("packet buffer too small")
-        check(lib().e2sar_hip_segment_batch(
-            self.ctx.handle, C.c_void_p(plan.device.data_ptr()), plan.n_events,
-            plan.max_packets_per_event, self.lb_hdr_version, self.max_pld,
-            1 if plan.aligned4 else 0, C.c_void_p(packets.data_ptr()), self.stride,
-            C.c_void_p(lens.data_ptr() if lens is not None else 0),
-            C.c_void_p(_stream_handle(stream))))
+        common = (C.c_void_p(plan.device.data_ptr()), plan.n_events,
+                  plan.max_packets_per_event, self.lb_hdr_version, self.max_pld,
+                  1 if plan.aligned4 else 0, C.c_void_p(packets.data_ptr()), self.stride,
+                  C.c_void_p(lens.data_ptr() if lens is not None else 0))
+        if recycle is not None:
+            check(lib().e2sar_hip_segment_batch_recycle(self.ctx.handle, *common, recycle.handle, 1 if force else 0,
+                                                        C.c_void_p(_stream_handle(stream))))
+        else:
+            check(lib().e2sar_hip_segment_batch(self.ctx.handle, *common, C.c_void_p(_stream_handle(stream))))
         return plan.total_packets
 
     def segment_reassemble(self, plan: SegPlan, packets: torch.Tensor, lens: torch.Tensor,

@@ -307,6 +307,17 @@ int e2sar_hip_reas_get_stats(e2sar_hip_reas *r, e2sar_hip_reas_stats *out);
  * promises it no longer reads event bytes from the arena.  `force` drops in-progress
  * events without logging them.  Asynchronous. */
 int e2sar_hip_reas_recycle(e2sar_hip_reas *r, int force, void *stream);
+/* e2sar_hip_segment_batch and e2sar_hip_reas_recycle(r, force) in ONE launch: extra
+ * workgroups at the end of the segmentation grid reset r's table and arena (no seg block
+ * touches them).  Same preconditions as the two calls; r's earlier launches on `stream`
+ * finish before it starts, and its next reassembly starts after it.  What it saves is one
+ * launch and its boundary per step (the bench's step: recycle, then segment -> reassemble
+ * per batch).  Replaces nothing in the reference (whose events are new[] buffers); see
+ * e2sar_hip_reas_recycle. */
+int e2sar_hip_segment_batch_recycle(e2sar_hip_ctx *ctx, const e2sar_hip_seg_event *d_events, uint32_t nEvents,
+                                    uint32_t maxPacketsPerEvent, int lbHdrVersion, uint32_t maxPldLen,
+                                    int eventsDwordAligned, uint8_t *d_packets, uint32_t stride, uint32_t *d_lens,
+                                    e2sar_hip_reas *r, int force, void *stream);
 /* Streaming form of recycle: move every in-progress event (its table entry and the
  * bytes received so far) to the alternate table/arena, which becomes current; the old
  * arena is free again.  Needs E2SAR_HIP_REAS_COMPACTABLE, and every completed record

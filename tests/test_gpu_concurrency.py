@@ -149,9 +149,12 @@ def test_two_streams_one_reassembler(hip, mtu, n_ev, a_first):
     assert overlapped[-1][0], f"the two streams never ran together: {overlapped}"
 
 
-def test_bench_scale_graph_roundtrip(hip):
+@pytest.mark.parametrize("fold", [False, True])
+def test_bench_scale_graph_roundtrip(hip, fold):
     """bench.py's headline step (config 2) as a suite test: 1024 x 1 MiB at MTU 1500, five
-    205-event batches, four steps per captured graph, three replays, all verified."""
+    205-event batches, four steps per captured graph, three replays, all verified.  fold:
+    the step's recycle runs inside its first segmentation launch
+    (e2sar_hip_segment_batch_recycle), as bench.py's default step does."""
     torch = _torch()
     from e2sar_amd import sar
     B, E, BATCH, STEPS, REPLAYS = 1 << 20, 1024, 205, 4, 3
@@ -166,9 +169,13 @@ def test_bench_scale_graph_roundtrip(hip):
                               lost_capacity=1024, arena_bytes=E * B + 4096)
 
     def step():
-        R.recycle(force=True)
-        for p in plans:
-            seg.segment(p, pk, ln)
+        if not fold:
+            R.recycle(force=True)
+        for k, p in enumerate(plans):
+            if k == 0 and fold:
+                seg.segment(p, pk, ln, recycle=R, force=True)
+            else:
+                seg.segment(p, pk, ln)
             R.reassemble(pk, stride, ln, p.total_packets)
 
     # the oracle's counters for one event's datagrams (the stream is E such events in order)
@@ -271,3 +278,41 @@ def test_context_destroyed_before_its_reassembler(hip):
             ctx.close()
         x = torch.full((64,), 7, dtype=torch.int32, device=hip.torch_device)
         assert torch.equal(x, x.clone())                          # the process is still healthy
+
+
+def test_segment_batch_recycle_preconditions(hip):
+    """e2sar_hip_segment_batch_recycle without force refuses as e2sar_hip_reas_recycle does
+    (completed records not yet polled), and once polled it segments and recycles in one launch:
+    the arena and table are empty again and the next reassembly starts from offset 0."""
+    torch = _torch()
+    from e2sar_amd import sar
+    B, n_ev = 100_000, 4
+    src = _source(hip, n_ev, B, 0xACE)
+    seg, plan, pk, ln = _segment(hip, src, B, 1500)
+    stride, n = seg.stride, plan.total_packets
+    R = sar.DeviceReassembler(hip, with_lb_header=True, table_slots=64, arena_bytes=n_ev * B + 4096)
+    R.reassemble(pk, stride, ln, n)
+    pk2, ln2 = seg.alloc_packets(n)
+    from e2sar_amd._capi import E2SARHipError
+    with pytest.raises(E2SARHipError):
+        seg.segment(plan, pk2, ln2, recycle=R, force=False)      # records not polled yet
+    first = R.poll()
+    assert len(first) == n_ev
+    st = R.stats()
+    assert st.arenaUsed > 0 and st.tableUsed == n_ev
+    seg.segment(plan, pk2, ln2, recycle=R, force=False)
+    torch.cuda.synchronize()
+    st = R.stats()
+    assert st.arenaUsed == 0 and st.tableUsed == 0 and st.inProgress == 0
+    assert torch.equal(ln2[:n], ln[:n])
+    a = pk[: n * stride].view(n, stride).cpu().numpy()
+    b = pk2[: n * stride].view(n, stride).cpu().numpy()
+    L = ln[:n].cpu().numpy()
+    assert all(np.array_equal(a[k, : L[k]], b[k, : L[k]]) for k in range(n))
+    R.reassemble(pk2, stride, ln2, n)
+    recs = R.poll()
+    assert sorted(r.eventNum for r in recs) == sorted(r.eventNum for r in first)
+    assert min(r.arenaOffset for r in recs) == 0
+    arena = R.arena_tensor()
+    for r in recs:
+        assert torch.equal(arena[r.arenaOffset: r.arenaOffset + B], src[r.eventNum, :B])

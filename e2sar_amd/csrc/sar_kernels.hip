@@ -1590,24 +1590,33 @@ __global__ __launch_bounds__(TB) void reas_scatter_classify_kernel(
 // key of a datagram that does not take part (bad header, bounds, table full): no real slot,
 // so it joins no run
 constexpr uint32_t kRoNoSlot = 0xFFFFFFFFu;
-constexpr uint32_t kWgKeys = 2u * kBlock;       // the key pass's per-workgroup key table
+// Key-pass workgroup: 1024 threads (round 6, profiles/round6/ro_keypass/): events
+// interleaved datagram by datagram put the same keys in every workgroup of their span, and
+// each workgroup registers a key and files its runs with one lookup and one returning atomic
+// on that key's slot -- 1024-datagram workgroups make 4x fewer of those than 256: K = 64 /
+// 205 interleaved events 190 / 425 -> 135-137 / 232-235 us per batch, K = 1 / 8 91.7-94.0 /
+// 117-118 -> 91.2-91.8 / 113-114 (512 threads: 144-146 / 290-292; 1024 threads with two
+// datagrams per lane, one workgroup per CU: 148-149 / 237 -- too few workgroups).
+constexpr int kRoKeyBlock = 1024;
 
-__global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
-                                                        const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
-                                                        RoScratch sc, PktInfo *__restrict__ info)
+template <int TB>
+__global__ __launch_bounds__(TB) void ro_key_kernel(ReasDev R, const uint8_t *__restrict__ pkts, uint32_t stride,
+                                                    const uint32_t *__restrict__ lens, uint32_t n, uint64_t now,
+                                                    RoScratch sc, PktInfo *__restrict__ info)
 {
-    // the workgroup's distinct keys (at most kBlock): one global lookup and one run-count
+    // the workgroup's distinct keys (at most TB): one global lookup and one run-count
     // atomic per key per workgroup, not per wave
+    constexpr uint32_t kWgKeys = 2u * TB;       // the per-workgroup key table
     __shared__ unsigned long long wgEv[kWgKeys];
     __shared__ uint32_t wgD[kWgKeys], wgTag[kWgKeys], wgCnt[kWgKeys], wgSlot[kWgKeys], wgBase[kWgKeys];
-    const uint32_t wave = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    const uint32_t wave = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     const uint32_t p0 = wave * 64u;
     const bool waveLive = p0 < n;                              // (a wave past n still meets the barriers)
     const uint32_t gn = !waveLive ? 0u : (n - p0 < 64u) ? n - p0 : 64u;
     const bool live = lane < gn;
     const uint32_t p = waveLive ? p0 + (live ? lane : 0u) : 0u;
-    for (uint32_t i = threadIdx.x; i < kWgKeys; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < kWgKeys; i += TB) {
         wgTag[i] = 0u;
         wgCnt[i] = 0u;
     }
@@ -1622,31 +1631,17 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         h.ok = false;
         h.derr = true;
     }
-    // runs of equal keys: only the run head takes part; of the run heads of one key in the
-    // wave (events interleaved in arrival make many), only the first registers the key and
-    // files the wave's runs of that key with one atomic.  The loop visits each distinct key
-    // of the wave once (usually one or two)
+    // runs of equal keys: only the run head takes part.  Every head registers its key in the
+    // workgroup's table itself and takes its run index there with one LDS atomic (round 6:
+    // a per-wave loop that first collapsed the heads of one key took 64 passes in a wave of
+    // 64 interleaved events; K = 64 / 205 136.5 / 233 -> 126.5 / 225 us per batch, in
+    // order unchanged, profiles/round6/ro_keypass/)
     const uint64_t pev = ((uint64_t)lane_prev((uint32_t)(h.ev >> 32), 0u) << 32) | lane_prev((uint32_t)h.ev, 0u);
     const uint32_t pd = lane_prev(h.d, 0u), pok = lane_prev(h.ok ? 1u : 0u, 0u);
     const bool head = h.ok && (lane == 0 || !pok || pev != h.ev || pd != h.d);
-    uint64_t same = 0;                                         // heads of this lane's key
-    uint32_t lead = lane;                                      // the first of them
-    for (uint64_t pend = __ballot(head); pend;) {              // wave-uniform
-        const uint32_t f = (uint32_t)__builtin_ctzll(pend);
-        const uint64_t fev = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(h.ev >> 32), (int)f) << 32) |
-                             (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)h.ev, (int)f);
-        const uint32_t fd = (uint32_t)__builtin_amdgcn_readlane((int)h.d, (int)f);
-        const uint64_t m = __ballot(head && h.ev == fev && h.d == fd);
-        if ((m >> lane) & 1ull) {
-            same = m;
-            lead = f;
-        }
-        pend &= ~m;
-    }
-    const bool leader = head && lead == lane;
-    // each wave's leaders claim or find their key's entry in the workgroup's table
+    // each head claims or finds its key's entry in the workgroup's table
     uint32_t e = slot_hash(h.ev, h.d, kWgKeys - 1u);
-    bool pending = leader, check = false;
+    bool pending = head, check = false;
     __syncthreads();                                           // table cleared
     while (__syncthreads_or(pending)) {
         if (pending) {
@@ -1665,11 +1660,11 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
             else e = (e + 1u) & (kWgKeys - 1u);
         }
     }
-    // this wave's runs of the key (its heads): their offset among the workgroup's runs of it
+    // this head's run: its index among the workgroup's runs of the key
     uint32_t o = 0;
-    if (leader) o = atomicAdd(&wgCnt[e], (uint32_t)__builtin_popcountll(same));
+    if (head) o = atomicAdd(&wgCnt[e], 1u);
     __syncthreads();
-    for (uint32_t b = 0; b < kWgKeys; b += kBlock) {           // one lookup + one atomic per key
+    for (uint32_t b = 0; b < kWgKeys; b += TB) {               // one lookup + one atomic per key
         const uint32_t i = b + threadIdx.x;
         const bool want = wgTag[i] != 0u;
         const LookupResult lr = find_or_create<true>(R, want, wgEv[i], wgD[i], 0u, now);
@@ -1679,14 +1674,13 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         }
     }
     __syncthreads();
-    const uint32_t lslot = leader ? wgSlot[e] : kNoSlot;
-    const uint32_t lkb = leader ? wgBase[e] + o : 0u;
+    const uint32_t hslot = head ? wgSlot[e] : kNoSlot;
+    const uint32_t k = head ? wgBase[e] + o : 0u;            // this run's index in its key
     const uint64_t H = __ballot(head);
     const uint64_t le = (lane == 63) ? ~0ull : ((2ull << lane) - 1ull);
     const uint64_t hm = H & le;
     const int myhead = hm ? 63 - __builtin_clzll(hm) : (int)lane;
-    const uint32_t keyLead = __shfl(lead, myhead);
-    const uint32_t slot = __shfl(lslot, (int)keyLead);
+    const uint32_t slot = __shfl(hslot, myhead);
     if (h.ok && slot == kNoSlot) {                             // table full / probe timeout
         h.ok = false;
         h.derr = true;
@@ -1696,22 +1690,16 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
         st16(reinterpret_cast<uint8_t *>(sc.recs + p), v);
         if (!h.ok) st16(reinterpret_cast<uint8_t *>(info + p), u32x4{0u, 0u, 0u, hl});   // takes no part
     }
-    // runs of consecutive positions of one key (one slot) within the wave, filed in the
-    // slot's bucket (the first run of a slot in the batch lists the slot for the walk)
+    // runs of consecutive positions of one key (one slot) within the wave -- they start at
+    // the heads -- filed in the slot's bucket (the run of index 0 lists the slot for the walk)
     const uint32_t ks = h.ok ? slot : kRoNoSlot;
     const uint32_t pks = lane_prev(ks, kRoNoSlot), nks = lane_next(ks, kRoNoSlot);
     const bool rhead = h.ok && (lane == 0 || pks != ks);
     const bool rtail = h.ok && (lane == 63 || nks != ks);
     const uint64_t RT = __ballot(rtail);
-    // the wave's runs of one key take consecutive indices k (in lane order) from the
-    // workgroup's block of the key (runs and heads coincide: a run starts at a head)
-    const uint64_t RH = __ballot(rhead);
-    const uint64_t myRuns = same & RH;
-    const uint32_t kb = (uint32_t)__shfl((int)lkb, (int)lead);
     if (rhead) {
         const uint64_t below = (1ull << lane) - 1ull;
         const uint32_t len = (uint32_t)__builtin_ctzll(RT & ~below) - lane + 1u;   // to this run's last lane
-        const uint32_t k = kb + (uint32_t)__builtin_popcountll(myRuns & below);
         if (k == 0u) sc.active[atomicAdd(&sc.ctr[1], 1u)] = slot;
         if (k < kRoBucket) {
             sc.bucket[(size_t)slot * kRoBucket + k] = ((unsigned long long)p << 32) | len;
@@ -1721,7 +1709,7 @@ __global__ __launch_bounds__(kBlock) void ro_key_kernel(ReasDev R, const uint8_t
     }
     // which lanes of this wave hold an overflow run (every wave writes its word; a flag tells
     // the place pass to look -- a plain store, not a counter all waves would contend on)
-    const uint64_t OV = __ballot(rhead && kb + (uint32_t)__builtin_popcountll(myRuns & ((1ull << lane) - 1ull)) >= kRoBucket);
+    const uint64_t OV = __ballot(rhead && k >= kRoBucket);
     if (lane == 0 && waveLive) {
         sc.ovMask[wave] = OV;
         if (OV) sc.ctr[0] = 1u;
@@ -2800,8 +2788,8 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     uint8_t *w = static_cast<uint8_t *>(work);
     PktInfo *info = reinterpret_cast<PktInfo *>(w);
     const RoScratch sc = ro_scratch_layout(scratch, n, R.tableSlots);
-    hipLaunchKernelGGL(ro_key_kernel, dim3(cdiv(n, kBlock)), dim3(kBlock), 0, stream, R, pkts, stride, lens, n, now,
-                       sc, info);
+    hipLaunchKernelGGL((ro_key_kernel<kRoKeyBlock>), dim3(cdiv(n, (uint32_t)kRoKeyBlock)), dim3(kRoKeyBlock), 0, stream,
+                       R, pkts, stride, lens, n, now, sc, info);
     hipLaunchKernelGGL(ro_place_kernel, dim3(kPlaceBlocks), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots, n);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;

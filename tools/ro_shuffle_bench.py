@@ -31,6 +31,8 @@ def main():
     ap.add_argument("--windows", default="1,8,64,0")
     ap.add_argument("--interleave", default="1")
     ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--extra-flags", type=lambda v: int(v, 0), default=0,
+                    help="A/B: e2sar_hip_reas_config.flags bits OR'd in (bits 16..: ReasDev.abForm)")
     args = ap.parse_args()
 
     import torch
@@ -57,7 +59,7 @@ def main():
         table <<= 1
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=table, queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
-                              flags=_capi.REAS_REFERENCE_ORDER)
+                              flags=_capi.REAS_REFERENCE_ORDER | args.extra_flags)
     pk2, ln2 = seg.alloc_packets(n)
     algo = E * (2 * B + 36 * npk)
     cases = [(int(w), int(k)) for w in args.windows.split(",") for k in args.interleave.split(",")]

@@ -1790,6 +1790,11 @@ __global__ __launch_bounds__(kPlaceThreads) void ro_place_kernel(RoScratch sc, u
 // offset-0 fragments and replays after completion add segments.
 constexpr uint32_t kRoAhead = 4;
 constexpr uint32_t kRoSortLds = 2048;       // runs of one key sorted in LDS by its wave (16 KiB)
+// The walk runs one wave per workgroup with 32 KiB of LDS (round 6, profiles/round6/ro_walk/):
+// four key waves per workgroup sharing a CU, 16 KiB each, left three quarters of the CUs
+// idle and sent keys whose span outgrew a 16 KiB position bitmap to the run sort -- 205
+// events interleaved 224 -> 151 us per batch, in order and K = 8 / 64 about 1 us faster.
+constexpr uint32_t kRoWalkLds = 4096;       // 8-byte words of LDS per walk wave
 
 // Bitonic sort of P = 128 NP keys in LDS by one wave: per stage each lane loads its NP
 // pairs at once (one LDS round trip per stage, not one per pair), then compares and stores.
@@ -1889,7 +1894,7 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v)
 // key's span (LDS atomic ORs), and the set bits read in order are the positions.  Returns
 // how many (0 when bitmap and list do not fit the region: then the runs are sorted).
 __device__ uint32_t ro_positions(const RoScratch &sc, uint32_t slot, uint32_t c, unsigned long long bv,
-                                 unsigned long long *lds, uint32_t lane)
+                                 unsigned long long *lds, uint32_t lane, uint32_t ldsWords)
 {
     const unsigned long long *ov = sc.placed + sc.runBase[slot];
     uint32_t mn = 0xFFFFFFFFu, mx = 0, tl = 0;
@@ -1904,7 +1909,7 @@ __device__ uint32_t ro_positions(const RoScratch &sc, uint32_t slot, uint32_t c,
     mx = wave_max_u32(mx);
     tl = (uint32_t)__builtin_amdgcn_readlane((int)wave_incl_scan(tl), 63);
     const uint32_t words = (mx - mn + 63u) / 64u;
-    if ((size_t)words * 8u + (size_t)tl * 4u > (size_t)kRoSortLds * 8u) return 0u;   // wave-uniform
+    if ((size_t)words * 8u + (size_t)tl * 4u > (size_t)ldsWords * 8u) return 0u;     // wave-uniform
     for (uint32_t i = lane; i < words; i += 64u) lds[i] = 0ull;
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();
@@ -1945,11 +1950,15 @@ __device__ uint32_t ro_positions(const RoScratch &sc, uint32_t slot, uint32_t c,
     return tl;
 }
 
-__global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc, uint32_t T, uint64_t now,
-                                                         PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
+// WB waves per workgroup, LW 8-byte words of LDS per wave (the position bitmap and list, or
+// the LDS sort of <= kRoSortLds runs)
+template <int WB, uint32_t LW>
+__global__ __launch_bounds__(WB * 64) void ro_walk_kernel(ReasDev R, RoScratch sc, uint32_t T, uint64_t now,
+                                                          PktInfo *__restrict__ info, FinishRec *__restrict__ fin)
 {
-    __shared__ unsigned long long roSort[kBlock / 64][kRoSortLds];
-    const uint32_t w = blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+    static_assert(LW >= kRoSortLds, "the LDS sort needs kRoSortLds words");
+    __shared__ unsigned long long roSort[WB][LW];
+    const uint32_t w = blockIdx.x * (uint32_t)WB + (threadIdx.x >> 6);
     const uint32_t lane = threadIdx.x & 63u;
     // the chain of dependent loads before the walk proper is kept short: the key is read
     // beside the count of keys, and its bucket beside its run count
@@ -1964,7 +1973,7 @@ __global__ __launch_bounds__(kBlock) void ro_walk_kernel(ReasDev R, RoScratch sc
     const unsigned long long *runsOf = nullptr;
     uint32_t nPos = 0;                                         // > 0: the key's positions are in lds
     if (!inBucket) {
-        nPos = ro_positions(sc, slot, nRuns, bv, lds, lane);
+        nPos = ro_positions(sc, slot, nRuns, bv, lds, lane, LW);
         if (nPos == 0u) runsOf = ro_sort_runs(sc, slot, nRuns, bv, lds, lane);
     }
     const RoRec *__restrict__ recs = sc.recs;
@@ -2793,7 +2802,7 @@ hipError_t launch_ro_classify(const ReasDev &R, const uint8_t *pkts, uint32_t st
     hipLaunchKernelGGL(ro_place_kernel, dim3(kPlaceBlocks), dim3(kPlaceThreads), 0, stream, sc, R.tableSlots, n);
     // one wave per key: at most min(n, tableSlots) keys
     const uint32_t waves = n < R.tableSlots ? n : R.tableSlots;
-    hipLaunchKernelGGL(ro_walk_kernel, dim3(cdiv(waves, kBlock / 64)), dim3(kBlock), 0, stream, R, sc, R.tableSlots, now, info,
+    hipLaunchKernelGGL((ro_walk_kernel<1, kRoWalkLds>), dim3(waves), dim3(64), 0, stream, R, sc, R.tableSlots, now, info,
                        reinterpret_cast<FinishRec *>(w + work_fin_off(n)));
     return hipGetLastError();
 }

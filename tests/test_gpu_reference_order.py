@@ -265,12 +265,15 @@ def test_interleaved_events_many_runs(hip, nev, ev_bytes, slots):
         assert lost == rlost and loss == rloss and inp == rinp, mode
 
 
-@pytest.mark.parametrize("nev,ev_bytes", [(160, 1 << 20), (28, 3 << 20)])
-def test_interleaved_wide_span_sorts_runs(hip, nev, ev_bytes):
-    """Many events interleaved datagram by datagram: a key's span is too wide for the walk
-    wave's position bitmap, so its runs are sorted -- 160 x 1 MiB (731 runs per key) by the
-    bitonic wave sort in LDS, 28 x 3 MiB (2192 runs per key) in global memory."""
-    mp = O.max_pld_len(1500)
+@pytest.mark.parametrize("nev,ev_bytes,mtu", [(160, 1 << 20, 1500), (360, 731 * 16, 80), (100, 2200 * 16, 80)])
+def test_interleaved_wide_span_sorts_runs(hip, nev, ev_bytes, mtu):
+    """Many events interleaved datagram by datagram: a key's span is wide.  160 x 1 MiB (731
+    runs per key over ~117 K positions): the walk wave's position bitmap (32 KiB of LDS per
+    wave since round 6).  At MTU 80 (16-byte payloads, 64-byte slots) spans too wide for the
+    bitmap: 360 events of 731 datagrams (~263 K positions) sort their runs with the bitonic
+    wave sort in LDS; 100 events of 2200 datagrams (more than 2048 runs per key) in global
+    memory."""
+    mp = O.max_pld_len(mtu)
     stride = (36 + mp + 15) // 16 * 16
     pks, lns = [], []
     for k in range(nev):
@@ -283,7 +286,8 @@ def test_interleaved_wide_span_sorts_runs(hip, nev, ev_bytes):
     ref, rst, rlost, rloss, rinp = _oracle(pk, ln)
     n = len(ln)
     # one batch: the whole span in one walk (a cut would leave each batch's span narrow enough)
-    got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, n], "fused", arena=nev * ev_bytes + (8 << 20), slots=1024)
+    got, st, lost, loss, inp = _gpu(hip, pk, ln, stride, [0, n], "fused", arena=nev * ev_bytes + (8 << 20),
+                                    slots=1024 if nev <= 512 else 2048)
     assert st == rst, (st, rst)
     assert sorted(got) == sorted(ref) and len(ref) == nev
     for k in ref:

@@ -90,9 +90,6 @@ def parse(argv=None):
     ap.add_argument("--fold-recycle", type=int, default=1,
                     help="1: the step's table/arena recycle runs inside its first seg_kernel launch "
                          "(e2sar_hip_segment_batch_recycle); 0: a reas_recycle_kernel launch of its own")
-    ap.add_argument("--reas-flags", type=lambda v: int(v, 0), default=0,
-                    help="A/B: extra e2sar_hip_reas_config.flags bits for the headline reassembler "
-                         "(bits 16..: launch-form A/B bits, ReasDev.abForm)")
     ap.add_argument("--reas-group", type=int, default=0,
                     help="A/B: datagrams per fused-reassembly workgroup (1..64; 0 = the library's balanced choice)")
     ap.add_argument("--table-factor", type=int, default=8,
@@ -538,7 +535,7 @@ def run_workload(args, env, headline: bool):
     from e2sar_amd import _capi
     R = sar.DeviceReassembler(ctx, with_lb_header=True, table_slots=max(table, 64), queue_capacity=E + 64,
                               lost_capacity=1024, arena_bytes=E * ev_stride + 4096,
-                              flags=(_capi.REAS_REFERENCE_ORDER if args.reference_order else 0) | args.reas_flags,
+                              flags=_capi.REAS_REFERENCE_ORDER if args.reference_order else 0,
                               group_size=args.reas_group)
     if args.landing == "spread":
         R.set_owner(world, rank)          # reassemble only this rank's events (eventNum % world)

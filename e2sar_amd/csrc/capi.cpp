@@ -544,7 +544,6 @@ int e2sar_hip_reas_create(e2sar_hip_ctx *ctx, const e2sar_hip_reas_config *cfg, 
     r->dev.ownWorld = 1;                       // every event is ours until set_owner
     r->dev.ownSelf = 0;
     r->dev.groupSize = cfg->groupSize;
-    r->dev.abForm = cfg->flags >> 16;          // A/B launch-form bits
     r->alt = r->dev;
     r->alt.arena = nullptr;
     if (cfg->flags & E2SAR_HIP_REAS_COMPACTABLE) {

@@ -103,7 +103,6 @@ struct ReasDev {
     uint32_t ownWorld;
     uint32_t ownSelf;
     uint32_t groupSize;       // datagrams per reas_kernel workgroup (config), 0 = chip-balanced auto
-    uint32_t abForm;          // A/B launch-form bits (e2sar_hip_reas_config.flags >> 16)
 };
 
 // Per-datagram result of classification (held in LDS between the two phases of reas_kernel).

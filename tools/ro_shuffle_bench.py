@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--interleave", default="1")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--extra-flags", type=lambda v: int(v, 0), default=0,
-                    help="A/B: e2sar_hip_reas_config.flags bits OR'd in (bits 16..: ReasDev.abForm)")
+                    help="e2sar_hip_reas_config.flags bits OR'd in (e.g. 4: E2SAR_HIP_REAS_COLD_DATAGRAMS)")
     args = ap.parse_args()
 
     import torch

@@ -69,3 +69,32 @@ def test_config1_cpu_loopback_runs():
     out = subprocess.run([exe, "65536", "1500", "1"], capture_output=True, text=True, timeout=60, check=True)
     res = json.loads(out.stdout.strip().splitlines()[-1])
     assert res["events"] > 0 and res["bad_events"] == 0 and res["GiBps"] > 0
+
+
+def test_abandoned_sub_leg_prints_one_line_and_exits_nonzero(tmp_path):
+    """A sub-leg that fails or stalls at N > 1: rank 0 prints the run's line once (the
+    headline plus the sub-leg's error), even when the deadline timer's thread and the main
+    thread both reach the print, and the process exits with status 3 so torchrun / CI see it."""
+    import json
+    import subprocess
+    prog = tmp_path / "abandon.py"
+    prog.write_text(
+        "import sys, threading\n"
+        f"sys.path.insert(0, {ROOT!r})\n"
+        "import bench\n"
+        "line = {'metric': 'm', 'value': 1.0}\n"
+        "bench._print_line(line)\n"                       # the main thread printed already
+        "t = threading.Thread(target=bench._abandon_sub_leg, args=(line, 'spread', 0, 'stalled'))\n"
+        "t.start(); t.join()\n")
+    r = subprocess.run([sys.executable, str(prog)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3, (r.returncode, r.stderr[-500:])
+    out = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(out) == 1 and json.loads(out[0]) == {"metric": "m", "value": 1.0}
+    assert "sub-leg spread abandoned (stalled)" in r.stderr
+    prog2 = tmp_path / "abandon2.py"
+    prog2.write_text(
+        f"import sys\nsys.path.insert(0, {ROOT!r})\nimport bench\n"
+        "bench._abandon_sub_leg({'metric': 'm', 'value': 2.0}, 'spread', 0, 'RuntimeError: x')\n")
+    r = subprocess.run([sys.executable, str(prog2)], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 3
+    assert json.loads(r.stdout.strip()) == {"metric": "m", "value": 2.0, "spread": {"error": "RuntimeError: x"}}

@@ -1040,6 +1040,9 @@ __device__ __forceinline__ void da_store(const PktInfo pi, uint32_t c, u32x4 x, 
     }
 }
 
+// The fused kernel's store windows start on this many 16-byte blocks (one 128-byte line)
+constexpr uint32_t kWinAlign = 8;
+
 // Per-workgroup LDS of the fused reassembly: destinations of the group's datagrams, and
 // the run tails' completion state (only the atomic's return value stays in registers during
 // the copy, which keeps the kernel's occupancy up).
@@ -1075,23 +1078,35 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
     TRACE_WAIT();
     TRACE_AT(2, 0, trace_now());
 
+    // Index space: datagram p owns S = spc + 14 rounded down to 8 positions, and its
+    // destination-aligned chunk c sits at position p * S + f + c, f = its destination's
+    // 16-byte block within a 128-byte line (dst mod 128 = bufferOffset mod 128: event
+    // buffers are 256-byte aligned).  Position ≡ destination block (mod 8), so every wave's
+    // 64 positions store whole 128-byte lines at both ends of its window.  With one position
+    // per chunk (S = spc), a window started and ended inside a line, the neighbouring
+    // window's store instruction wrote the rest later, and the non-temporal lines left L2 in
+    // between: 1.044x the payload in writes, 103 K partial write requests per launch; here
+    // 1.003x and 16 K (profiles/round6/window_align/: reas_kernel at MTU 9000 68.2-68.8 vs
+    // 69.9-70.8 us, at 1500 72.0-73.4 vs 72.8-74.6).  At MTU 1500 the padding costs no
+    // round: 59 datagrams fill 1.77 rounds of 3072 chunks at S = 92 and 2.0 at S = 104.
     const uint32_t spc = stride >> 4;
-    const uint32_t nch = gn * spc;
-    const float rspc = 1.0f / (float)spc;
+    const uint32_t S = (spc + 2u * (kWinAlign - 1u)) & ~(kWinAlign - 1u);
+    const uint32_t nch = gn * S;
+    const float rS = 1.0f / (float)S;
     const uint8_t *const bpk = pkts + (uint64_t)g0 * stride;
     const __amdgpu_buffer_rsrc_t bpkR = brsrc(bpk);                     // HO loads only
     (void)bpkR;
-    // chunk i -> (datagram, chunk within it); recomputed at store time rather than kept
-    // live across the classification (register pressure sets this kernel's occupancy)
-    auto split_chunk = [&](uint32_t i, uint32_t &p, uint32_t &c) {
+    // position i -> (datagram, position within its S); recomputed at store time rather than
+    // kept live across the classification (register pressure sets this kernel's occupancy)
+    auto split_pos = [&](uint32_t i, uint32_t &p, uint32_t &j) {
         const uint32_t ic = (i < nch) ? i : 0u;
-        p = (uint32_t)((float)ic * rspc);
-        if (p * spc > ic) p--;
-        else if ((p + 1u) * spc <= ic) p++;
-        c = ic - p * spc;
+        p = (uint32_t)((float)ic * rS);
+        if (p * S > ic) p--;
+        else if ((p + 1u) * S <= ic) p++;
+        j = ic - p * S;
     };
     const uint32_t hl = R.withLB ? kLBREHdrLen : kREHdrLen;
-    const uint32_t gPhase = bswap32(raw.re.y) & 15u;
+    const uint32_t gPhase = bswap32(raw.re.y) & (16u * kWinAlign - 1u);   // dst mod 128
     uint32_t gPlen = (raw.len >= hl) ? ((raw.len < stride) ? raw.len : stride) - hl : 0u;
     if (R.ownWorld > 1u && re_valid(raw.re.x) &&
         foreign_event(R, ((uint64_t)bswap32(raw.re.w) << 32) | bswap32(raw.re4)))
@@ -1100,11 +1115,12 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
 #pragma unroll
         for (int u = 0; u < U; u++) {
             const uint32_t i = r0 + (uint32_t)u * NT + tx;
-            uint32_t p, c;
-            split_chunk(i, p, c);
-            const uint32_t a = __shfl(gPhase, (int)p), plen = __shfl(gPlen, (int)p);
+            uint32_t p, j;
+            split_pos(i, p, j);
+            const uint32_t ph = __shfl(gPhase, (int)p), plen = __shfl(gPlen, (int)p);
+            const uint32_t a = ph & 15u, f = ph >> 4, c = j - f;
             uint32_t off = 0, sh;
-            if (i < nch && 16u * c < a + plen && (a & 3u) == 0u) off = p * stride + da_window(c, a, hl, stride, sh);
+            if (i < nch && j >= f && 16u * c < a + plen && (a & 3u) == 0u) off = p * stride + da_window(c, a, hl, stride, sh);
             xs[u] = HO ? ld16_sc1(bpkR, off) : ld16(bpk + off);
         }
     };
@@ -1113,9 +1129,12 @@ __device__ __forceinline__ void reas_range(const ReasDev &R, const uint8_t *__re
         for (int u = 0; u < U; u++) {
             const uint32_t i = r0 + (uint32_t)u * NT + tx;
             if (i >= nch) continue;
-            uint32_t p, c;
-            split_chunk(i, p, c);
-            da_store<HO>(L.info[p], c, xs[u], bpk + (uint64_t)p * stride, stride);
+            uint32_t p, j;
+            split_pos(i, p, j);
+            const PktInfo pi = L.info[p];
+            const uint32_t f = ((uint32_t)pi.dst >> 4) & (kWinAlign - 1u);
+            if (j < f) continue;
+            da_store<HO>(pi, j - f, xs[u], bpk + (uint64_t)p * stride, stride);
         }
     };
     u32x4 x[U], y[U];

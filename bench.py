@@ -47,6 +47,9 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--warm-timed", type=int, default=1,
+                    help="1: repeat the warmup steps (as the timed steps run: graph replays) right before "
+                         "the timed region's barrier; 0: only before verification and capture")
     ap.add_argument("--mtu", type=int, default=1500)
     ap.add_argument("--event-bytes", type=int, default=1 << 20)
     ap.add_argument("--events", type=int, default=1024, help="events per rank per step")
@@ -61,7 +64,8 @@ def parse(argv=None):
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--eager", action="store_true", help="launch from Python each step instead of a HIP graph")
     ap.add_argument("--graph-steps", type=int, default=0,
-                    help="steps captured in one HIP graph (0: the largest of 4, 2, 1 that divides --steps); "
+                    help="steps captured in one HIP graph (0: all --steps in one graph, up to 64; above that "
+                         "the largest divisor of --steps up to 64); "
                          "the timed region still runs exactly --steps steps")
     ap.add_argument("--overlap", action="store_true", help="reassemble batch b while segmenting b+1 (2 streams)")
     ap.add_argument("--xcd-groups", type=int, default=0,
@@ -255,11 +259,17 @@ def cpu_loopback(args, seconds: float):
 
 
 def graph_steps(args) -> int:
+    """Steps captured in one HIP graph.  Default: the whole timed region in one graph (up to 64
+    steps; above that the largest divisor of --steps up to 64).  Every graph launch costs the
+    GPU idle time at its start (the host submits its nodes), so fewer, longer graphs measure
+    the kernels rather than the launches: K = 20 with warm-timed replays, 20-step graph
+    1491-1495 GiB/s, 10-step 1450-1464, 4-step 1431-1443, 1-step 1397-1416; K = 200 in
+    4-step graphs 1496 (profiles/round6/timed_start/)."""
     if args.graph_steps > 0:
         if args.steps % args.graph_steps:
             raise SystemExit("--steps must be a multiple of --graph-steps")
         return args.graph_steps
-    return next(d for d in (4, 2, 1) if args.steps % d == 0)
+    return next(d for d in range(min(args.steps, 64), 0, -1) if args.steps % d == 0)
 
 def _pmc_traffic(args, dom, batch_events=None):
     """HBM traffic per launch of kernel `dom` from the committed rocprofv3 PMC summaries
@@ -777,14 +787,24 @@ def run_workload(args, env, headline: bool):
         if not args.no_verify:
             verified = verify() and verified is not False
 
-    def run_timed(fn, g, k):
-        """k steps (k/G graph replays, or k eager steps) between barriers; max over ranks."""
+    def run_timed(fn, g, k, gs=None):
+        """k steps (k/G graph replays, or k eager steps) between barriers; max over ranks.
+        With --warm-timed (default), the warmup steps are replayed once more right before the
+        barrier, the same way the timed steps run, so the timed region starts with the GPU in
+        the state the steps keep it in rather than after the verification's host work."""
+        if args.warm_timed and args.warmup > 0:
+            if g is not None:
+                for _ in range(-(-args.warmup // (gs or G))):
+                    g.replay()
+            else:
+                for _ in range(args.warmup):
+                    fn()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         if g is not None:
-            for _ in range(k // G):
+            for _ in range(k // (gs or G)):
                 g.replay()
         else:
             for _ in range(k):
@@ -925,9 +945,11 @@ def run_workload(args, env, headline: bool):
         cstep()
         torch.cuda.synchronize()
         cver = None if args.no_verify else verify()
-        cgraph = None if args.eager else capture(cstep, G)
-        ck = max(G, args.cold_steps // G * G)
-        cel = run_timed(cstep, cgraph, ck)
+        # the cold leg's own graph: all its --cold-steps in one graph (up to 64), as the step's
+        Gc = args.graph_steps or next(d for d in range(min(args.cold_steps, 64), 0, -1) if args.cold_steps % d == 0)
+        cgraph = None if args.eager else capture(cstep, Gc)
+        ck = max(Gc, args.cold_steps // Gc * Gc)
+        cel = run_timed(cstep, cgraph, ck, Gc)
         cper = kernel_times(cstep, args.roofline_steps)
         ckern = {"fused": "reas_kernel", "split": "reas_scatter_kernel",
                  "pipelined": "reas_scatter_classify_kernel"}[args.cold_reas]

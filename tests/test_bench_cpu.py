@@ -48,8 +48,10 @@ def test_gpus_n_starts_one_rank_per_gpu(monkeypatch):
 
 
 def test_graph_steps_divides_the_timed_steps():
-    for steps, g in ((20, 4), (10, 2), (7, 1), (5, 1)):
+    # the whole timed region in one graph up to 64 steps, else the largest divisor <= 64
+    for steps, g in ((20, 20), (10, 10), (7, 7), (5, 5), (64, 64), (100, 50), (200, 50), (67, 1), (130, 26)):
         assert bench.graph_steps(bench.parse(["--steps", str(steps)])) == g
+        assert steps % g == 0
     assert bench.graph_steps(bench.parse(["--steps", "6", "--graph-steps", "3"])) == 3
 
 

@@ -21,6 +21,10 @@ for w in $W; do
   mkdir -p $O/$w
   echo "== $w stats $(date +%T)" >> $O/progress.log
   timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$w/stats -o run -- python3 $R/bench.py --cpu-seconds 0 --steps 8 --warmup 1 $A > $O/$w/bench_profiled.json 2> $O/$w/stats.log
+  # the same workload launched eagerly (no graph): rocprof's per-dispatch overhead inflates
+  # the intervals of graph-replayed kernels, so kernel durations come from here
+  echo "== $w eager stats $(date +%T)" >> $O/progress.log
+  timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/$w/stats_eager -o run -- python3 $R/bench.py --cpu-seconds 0 --steps 8 --warmup 1 --eager $A > $O/$w/bench_profiled_eager.json 2> $O/$w/stats_eager.log
   echo "== $w pmc $(date +%T)" >> $O/progress.log
   timeout -k 10 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace --output-format csv -d $O/$w/fetch -o run -- python3 $R/bench.py --cpu-seconds 0 --steps 2 --warmup 1 --no-verify --eager $P > $O/$w/fetch.log 2>&1
   timeout -k 10 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace --output-format csv -d $O/$w/write -o run -- python3 $R/bench.py --cpu-seconds 0 --steps 2 --warmup 1 --no-verify --eager $P > $O/$w/write.log 2>&1

@@ -823,6 +823,9 @@ def run_workload(args, env, headline: bool):
     # ---- timed region ----
     K = args.steps
     elapsed = run_timed(step, graph, K)
+    # ...and the events the timed steps left behind, byte for byte (outside the timed region)
+    if not args.no_verify:
+        verified = verify() and verified is not False
 
     # ---- per-kernel durations: HIP events around each launch of the step, eager, on the
     # stream the kernels run on (the step is single-stream unless --overlap) ----
@@ -1034,6 +1037,9 @@ def run_workload(args, env, headline: bool):
                 "landing": args.landing,
                 "payload": args.payload,
                 "verified_roundtrip": verified,
+                "verified_at": None if args.no_verify else
+                ["an eager step", "the captured graph's first replay", "the timed steps' last step"]
+                if graph is not None else ["an eager step", "the timed steps' last step"],
             },
             "roofline": {
                 "bound": "hbm",
